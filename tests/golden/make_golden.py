@@ -1,0 +1,373 @@
+"""Generate golden input/output vectors by running the REFERENCE implementation.
+
+Run ONLY in the survey/build container, where /root/reference exists:
+
+    python tests/golden/make_golden.py
+
+It imports the reference (`yanerf.pipelines` from /root/reference) in-process
+with the small stand-ins under tests/golden/_stubs for third-party modules the
+image lacks (addict, yapf, imageio, omegaconf, cv2, torch._six). Every random
+draw the reference makes (torch.multinomial / rand_like / randn_like / rand) is
+recorded through a pass-through wrapper, so the fixtures hold the exact
+uniforms/normals the reference consumed and our kernels can be driven with the
+same values ("injected randomness" test mode).
+
+Outputs (data only: inputs + expected outputs) go to tests/golden/*.npz. The
+reference source never leaves /root/reference. Nothing in the GPU tests, bench
+or smoke() runs this script.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+import zlib
+from contextlib import contextmanager
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+REF = Path(os.environ.get("YANERF_REFERENCE", "/root/reference"))
+sys.path.insert(0, str(HERE / "_stubs"))
+sys.path.insert(0, str(REF))
+sys.path.insert(0, str(HERE))
+
+import torch  # noqa: E402
+
+_six = types.ModuleType("torch._six")
+_six.string_classes = (str, bytes)
+sys.modules.setdefault("torch._six", _six)
+
+from weights import LEGO_ARCH, SMALL_ARCH, checksum, make_nerf_mlp_params  # noqa: E402
+from scene import synthetic_pose  # noqa: E402
+
+from yanerf.pipelines.builder import PIPELINES  # noqa: E402
+from yanerf.pipelines.models import MODELS  # noqa: E402
+from yanerf.pipelines.models.utils import HarmonicEmbedding  # noqa: E402
+from yanerf.pipelines.ray_samplers import RAY_SAMPLERS  # noqa: E402
+from yanerf.pipelines.renderers import RENDERERS  # noqa: E402
+from yanerf.pipelines.renderers.multipass_emission_absorpsion_renderer import (  # noqa: E402
+    EmissionAbsorptionRaymarcher,
+)
+from yanerf.pipelines.renderers.utils import RayPointRefiner, sample_pdf  # noqa: E402
+from yanerf.pipelines.utils import EvaluationMode  # noqa: E402
+from yanerf.utils.config import Config  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+# ----------------------------------------------------------------------------- randomness capture
+class Recorder:
+    def __init__(self):
+        self.log = []
+
+    @contextmanager
+    def capture(self):
+        orig = {n: getattr(torch, n) for n in ("multinomial", "rand_like", "randn_like", "rand")}
+
+        def wrap(name):
+            f = orig[name]
+
+            def g(*a, **k):
+                out = f(*a, **k)
+                self.log.append((name, out.detach().clone()))
+                return out
+
+            return g
+
+        for n in orig:
+            setattr(torch, n, wrap(n))
+        try:
+            yield self
+        finally:
+            for n, f in orig.items():
+                setattr(torch, n, f)
+
+    def take(self, name):
+        return [t for (n, t) in self.log if n == name]
+
+
+def np32(t):
+    return t.detach().cpu().numpy().astype(np.float32)
+
+
+def build_mlp(arch, seed):
+    cfg = dict(type="NeRFMLP", **arch, harmonic_functions_xyz_append_intput=True,
+               harmonic_functions_dir_append_intput=True, latent_dim=0, input_xyz=True, input_dir=True)
+    model = MODELS.build(Config(dict(model=cfg)).model)
+    params = make_nerf_mlp_params(arch, seed)
+    sd = model.state_dict()
+    assert set(sd.keys()) == set(params.keys()), (sorted(sd.keys()), sorted(params.keys()))
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    return model, params
+
+
+# ----------------------------------------------------------------------------- cases
+def gen_harmonic(out):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(257, 3, generator=g) * 3.0
+    out["harmonic"] = dict(
+        x=np32(x),
+        xyz10=np32(HarmonicEmbedding(10, append_input=True)(x)),
+        dir4=np32(HarmonicEmbedding(4, append_input=True)(x)),
+        xyz8=np32(HarmonicEmbedding(8, append_input=True)(x)),
+    )
+
+
+def gen_raysampler(out):
+    g = torch.Generator().manual_seed(1)
+    for tag, cfg in (
+        ("small", dict(type="RaySampler", image_width=10, image_height=6, n_rays_per_image_sampled_from_mask=4,
+                       min_depth=0.5, max_depth=1.0, scene_extent=0.0, n_pts_per_ray_training=5,
+                       n_pts_per_ray_evaluation=5, stratified_point_sampling_training=True,
+                       stratified_point_sampling_evaluation=False)),
+        ("lego", dict(type="RaySampler", image_width=800, image_height=800, n_rays_per_image_sampled_from_mask=64,
+                      min_depth=2.0, max_depth=6.0, scene_extent=0.0, n_pts_per_ray_training=64,
+                      n_pts_per_ray_evaluation=64, stratified_point_sampling_training=True,
+                      stratified_point_sampling_evaluation=False)),
+    ):
+        rs = RAY_SAMPLERS.build(Config(dict(r=cfg)).r)
+        poses = torch.randn(2, 3, 4, generator=g)
+        focal = torch.tensor([500.0, 731.5])
+        d = dict(poses=np32(poses), focal=np32(focal))
+        # evaluation, configured grid (lego: override to 12x9 to keep the fixture small; quirk: principal point
+        # still uses the configured W/H, reference ray_sampler.py:236-246, 302-303)
+        kw = {} if tag == "small" else dict(image_height=9, image_width=12)
+        rb = rs(poses, focal, EvaluationMode.EVALUATION, **kw)
+        for k, v in rb._asdict().items():
+            d[f"eval_{k}"] = np32(v)
+        rb = rs(poses, focal, EvaluationMode.EVALUATION, image_height=3, image_width=6, min_depth=15.0, max_depth=30.0)
+        for k, v in rb._asdict().items():
+            d[f"evalov_{k}"] = np32(v)
+        rec = Recorder()
+        torch.manual_seed(5)
+        with rec.capture():
+            rb = rs(poses, focal, EvaluationMode.TRAINING)
+        d["train_pixel_ids"] = rec.take("multinomial")[0].numpy().astype(np.int64)
+        d["train_jitter_u"] = np32(rec.take("rand_like")[0])
+        for k, v in rb._asdict().items():
+            d[f"train_{k}"] = np32(v)
+        out[f"raysampler_{tag}"] = d
+
+
+def gen_mlp(out):
+    for tag, arch, seed, n_rays, P in (("small", SMALL_ARCH, 1, 6, 16), ("lego", LEGO_ARCH, 7, 4, 64)):
+        model, params = build_mlp(arch, seed)
+        g = torch.Generator().manual_seed(2)
+        o = torch.randn(2, n_rays // 2, 1, 3, generator=g) * 0.5 + torch.tensor([0.0, 0.0, 4.0])
+        dvec = torch.randn(2, n_rays // 2, 1, 3, generator=g)
+        dvec[..., 2] -= 1.5
+        t = torch.sort(torch.rand(2, n_rays // 2, 1, P, generator=g) * 4.0 + 2.0, dim=-1)[0]
+        res = model(o, dvec, t)
+        sig, rgb = res["rays_densities"], res["rays_features"]
+        gs = torch.randn(sig.shape, generator=g)
+        gc = torch.randn(rgb.shape, generator=g)
+        model.zero_grad()
+        ((sig * gs).sum() + (rgb * gc).sum()).backward()
+        d = dict(origins=np32(o), directions=np32(dvec), lengths=np32(t), sigma=np32(sig), rgb=np32(rgb),
+                 g_sigma=np32(gs), g_rgb=np32(gc), seed=np.int64(seed), checksum=checksum(params))
+        for name, p in model.named_parameters():
+            gr = np32(p.grad)
+            if gr.size <= 4096:
+                d[f"grad:{name}"] = gr
+            else:  # large weight grads: norm, sum and a fixed sample of entries
+                rng = np.random.Generator(np.random.PCG64(zlib.crc32(name.encode())))
+                idx = rng.choice(gr.size, size=512, replace=False)
+                d[f"gradidx:{name}"] = idx.astype(np.int64)
+                d[f"gradval:{name}"] = gr.reshape(-1)[idx]
+                d[f"gradsum:{name}"] = np.array([gr.astype(np.float64).sum(), np.linalg.norm(gr.astype(np.float64))])
+        out[f"mlp_{tag}"] = d
+
+
+def gen_raymarcher(out):
+    g = torch.Generator().manual_seed(3)
+    R, P = 37, 64
+    t = torch.sort(torch.rand(R, P, generator=g) * 4.0 + 2.0, dim=-1)[0]
+    dirs = torch.randn(R, 3, generator=g)
+    sig = torch.randn(R, P, 1, generator=g) * 3.0
+    sig[:5] -= 6.0  # mostly-empty rays
+    sig[5:9, 20:30] += 40.0  # hard surfaces
+    feats = torch.rand(R, P, 3, generator=g)
+    bg = torch.rand(R, 3, generator=g)
+    gf = torch.randn(R, 3, generator=g)
+    gd = torch.randn(R, 1, generator=g)
+    ga = torch.randn(R, 1, generator=g)
+    cases = [
+        ("blend0_bgdef", dict(blend_output=False), None, 0.0),
+        ("blend1_bgray", dict(blend_output=True), bg, 0.0),
+        ("blend0_noise", dict(blend_output=False), None, 0.2),
+        ("cap1_min", dict(blend_output=True, capping_function="cap1", weight_function="minimum"), bg, 0.0),
+        ("hardbg", dict(blend_output=False, hard_background=True), bg, 0.0),
+    ]
+    d = dict(lengths=np32(t), directions=np32(dirs), densities=np32(sig), features=np32(feats), bg=np32(bg),
+             g_features=np32(gf), g_depths=np32(gd), g_alpha=np32(ga))
+    for tag, kw, bgc, noise in cases:
+        rm = EmissionAbsorptionRaymarcher(surface_thickness=1, bg_color=(0.25, 0.5, 0.75),
+                                          background_density_bias=1e-6, **kw)
+        s = sig.clone().requires_grad_(True)
+        f = feats.clone().requires_grad_(True)
+        rec = Recorder()
+        torch.manual_seed(9)
+        with rec.capture():
+            feat, depth, alpha, w, _ = rm(s, f, {}, t, dirs, density_noise_std=noise, bg_color=bgc)
+        ((feat * gf).sum() + (depth * gd).sum() + (alpha * ga).sum()).backward()
+        if noise > 0:
+            d[f"{tag}:noise_n"] = np32(rec.take("randn_like")[0])
+        d[f"{tag}:features"] = np32(feat)
+        d[f"{tag}:depths"] = np32(depth)
+        d[f"{tag}:alpha"] = np32(alpha)
+        d[f"{tag}:weights"] = np32(w)
+        d[f"{tag}:g_densities"] = np32(s.grad)
+        d[f"{tag}:g_feats"] = np32(f.grad)
+    out["raymarcher"] = d
+
+
+def gen_sample_pdf(out):
+    g = torch.Generator().manual_seed(4)
+    R, P = 29, 64
+    z = torch.sort(torch.rand(R, P, generator=g) * 4.0 + 2.0, dim=-1)[0]
+    w = torch.rand(R, P, generator=g) ** 4
+    w[:3] = 0.0  # empty rays -> uniform pdf
+    w[3:6] = 0.0
+    w[3:6, 30] = 0.9  # single spike
+    d = dict(z=np32(z), w=np32(w))
+    bins = torch.lerp(z[..., 1:], z[..., :-1], 0.5)
+    d["bins"] = np32(bins)
+    d["det128"] = np32(sample_pdf(bins, w[..., 1:-1], 128, det=True))
+    d["det64"] = np32(sample_pdf(bins, w[..., 1:-1], 64, det=True))
+    rec = Recorder()
+    with rec.capture():
+        s = sample_pdf(bins, w[..., 1:-1], 128, det=False)
+    d["rand128_u"] = np32(rec.take("rand")[0])
+    d["rand128"] = np32(s)
+    for tag, rnd in (("det", False), ("rand", True)):
+        ref = RayPointRefiner(n_pts_per_ray=128, random_sampling=rnd, add_input_samples=True)
+        rec = Recorder()
+        with rec.capture():
+            rb = ref(torch.zeros(R, 3), torch.ones(R, 3), z, torch.zeros(R, 2), w)
+        if rnd:
+            d["refine_rand_u"] = np32(rec.take("rand")[0])
+        d[f"refine_{tag}"] = np32(rb.lengths)
+    out["sample_pdf"] = d
+
+
+def lego_pipeline_cfg(n_fine=128, noise=0.2, n_rays=4096, H=800, W=800, focal_img=800):
+    cfg = Config.fromfile(str(REF / "configs/nerf/lego.yml"))
+    p = cfg.pipeline
+    p.renderer.n_pts_per_ray_fine_training = n_fine
+    p.renderer.n_pts_per_ray_fine_evaluation = n_fine
+    p.renderer.density_noise_std_train = noise
+    p.ray_sampler.n_rays_per_image_sampled_from_mask = n_rays
+    p.ray_sampler.image_height = H
+    p.ray_sampler.image_width = W
+    return p
+
+
+def load_pipeline_weights(pipe, seeds):
+    for f, seed in zip(pipe.implicit_functions, seeds):
+        params = make_nerf_mlp_params(LEGO_ARCH, seed)
+        f._fn.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+
+
+def gen_render_eval(out):
+    pcfg = lego_pipeline_cfg()
+    pipe = PIPELINES.build(pcfg)
+    load_pipeline_weights(pipe, (11, 12))
+    pipe.eval()
+    pose = torch.from_numpy(synthetic_pose(30.0, -30.0, 4.0))[None]
+    focal = torch.tensor([1111.1111])
+    Hs, Ws = 16, 16
+    g = torch.Generator().manual_seed(6)
+    img = torch.rand(1, Hs, Ws, 3, generator=g)
+    with torch.no_grad():
+        preds = pipe(poses=pose, focal_lengths=focal, image_rgb=img, image_height=Hs, image_width=Ws,
+                     evaluation_mode=EvaluationMode.EVALUATION)
+    d = dict(pose=np32(pose), focal=np32(focal), image_rgb=np32(img), H=np.int64(Hs), W=np.int64(Ws),
+             seeds=np.array([11, 12]))
+    for k, v in preds.items():
+        if torch.is_tensor(v):
+            d[k] = np32(v)
+    # per-stage raw renderer outputs (both passes), through the renderer directly
+    rb = pipe.ray_sampler(pose, focal, evaluation_mode=EvaluationMode.EVALUATION, image_height=Hs, image_width=Ws)
+    with torch.no_grad():
+        ro = pipe.renderer(*rb, bg_color=None, implicit_functions=pipe.implicit_functions,
+                           evaluation_mode=EvaluationMode.EVALUATION)
+    d["fine_features"], d["fine_depths"], d["fine_alpha"] = np32(ro.features), np32(ro.depths), np32(ro.alpha_masks)
+    pv = ro.prev_stage
+    d["coarse_features"], d["coarse_depths"], d["coarse_alpha"] = np32(pv.features), np32(pv.depths), np32(pv.alpha_masks)
+    d["coarse_weights"] = np32(pv.aux["weights"])
+    d["fine_weights"] = np32(ro.aux["weights"])
+    out["render_eval_lego"] = d
+
+
+def gen_train_step(out):
+    n_rays = 48
+    pcfg = lego_pipeline_cfg(n_rays=n_rays)
+    pipe = PIPELINES.build(pcfg)
+    load_pipeline_weights(pipe, (21, 22))
+    pipe.train()
+    pose = torch.from_numpy(synthetic_pose(-60.0, -20.0, 4.0))[None]
+    focal = torch.tensor([1111.1111])
+    g = torch.Generator().manual_seed(8)
+    img = torch.rand(1, 800, 800, 3, generator=g)
+    rec = Recorder()
+    torch.manual_seed(10)
+    with rec.capture():
+        preds = pipe(poses=pose, focal_lengths=focal, image_rgb=img, evaluation_mode=EvaluationMode.TRAINING)
+    preds["objective"].mean().backward()
+    ids = rec.take("multinomial")[0].numpy().astype(np.int64)
+    d = dict(pose=np32(pose), focal=np32(focal), seeds=np.array([21, 22]), n_rays=np.int64(n_rays),
+             pixel_ids=ids, gt_rgb=np32(img.reshape(1, -1, 3)[0, ids[0]]),
+             jitter_u=np32(rec.take("rand_like")[0]),
+             noise_coarse=np32(rec.take("randn_like")[0]), noise_fine=np32(rec.take("randn_like")[1]),
+             pdf_u=np32(rec.take("rand")[0]))
+    for k in ("objective", "loss_rgb_mse", "loss_prev_stage_rgb_mse", "loss_rgb_huber"):
+        d[k] = np32(preds[k])
+    for i, f in enumerate(pipe.implicit_functions):
+        for name, p in f._fn.named_parameters():
+            gr = np32(p.grad)
+            if gr.size <= 4096:
+                d[f"grad{i}:{name}"] = gr
+            else:
+                d[f"gradsum{i}:{name}"] = np.array([gr.astype(np.float64).sum(), np.linalg.norm(gr.astype(np.float64))])
+                rng = np.random.Generator(np.random.PCG64(len(name) * 1000 + i))
+                idx = rng.choice(gr.size, size=256, replace=False)
+                d[f"gradidx{i}:{name}"] = idx.astype(np.int64)
+                d[f"gradval{i}:{name}"] = gr.reshape(-1)[idx]
+    out["train_step_lego"] = d
+
+
+def gen_zero_outputer(out):
+    """Known-answer (reference tests/test_pipeline.py:67-151): zero density -> rendered == bg exactly."""
+    pcfg = lego_pipeline_cfg(n_rays=4)
+    pcfg.model = dict(type="ZeroOutputer")
+    pcfg.renderer.blend_output = True
+    pcfg.renderer.density_noise_std_train = 0.0
+    pcfg.ray_sampler.image_height = 6
+    pcfg.ray_sampler.image_width = 10
+    pipe = PIPELINES.build(pcfg)
+    g = torch.Generator().manual_seed(12)
+    poses = torch.randn(3, 3, 4, generator=g)
+    focal = torch.ones(3) * 500
+    bg = torch.randn(3, 2, 4, 3, generator=g)
+    preds = pipe(poses=poses, focal_lengths=focal, bg_image_rgb=bg, image_rgb=bg,
+                 evaluation_mode=EvaluationMode.EVALUATION, image_width=4, image_height=2)
+    out["zero_outputer"] = dict(poses=np32(poses), focal=np32(focal), bg=np32(bg),
+                                rendered_images=np32(preds["rendered_images"]), objective=np32(preds["objective"]))
+
+
+def main():
+    out = {}
+    for f in (gen_harmonic, gen_raysampler, gen_mlp, gen_raymarcher, gen_sample_pdf, gen_render_eval,
+              gen_train_step, gen_zero_outputer):
+        f(out)
+        print("generated", f.__name__)
+    for name, d in out.items():
+        path = HERE / f"{name}.npz"
+        np.savez_compressed(path, **d)
+        print(f"{path.name}: {path.stat().st_size / 1024:.1f} KiB")
+
+
+if __name__ == "__main__":
+    main()

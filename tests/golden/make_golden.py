@@ -344,6 +344,7 @@ def gen_zero_outputer(out):
     pcfg.model = dict(type="ZeroOutputer")
     pcfg.renderer.blend_output = True
     pcfg.renderer.density_noise_std_train = 0.0
+    pcfg.renderer.background_density_bias = 0.0  # as the reference test's renderer config
     pcfg.ray_sampler.image_height = 6
     pcfg.ray_sampler.image_width = 10
     pipe = PIPELINES.build(pcfg)
@@ -353,6 +354,7 @@ def gen_zero_outputer(out):
     bg = torch.randn(3, 2, 4, 3, generator=g)
     preds = pipe(poses=poses, focal_lengths=focal, bg_image_rgb=bg, image_rgb=bg,
                  evaluation_mode=EvaluationMode.EVALUATION, image_width=4, image_height=2)
+    assert torch.all(preds["rendered_images"] == bg), "reference known answer must hold"
     out["zero_outputer"] = dict(poses=np32(poses), focal=np32(focal), bg=np32(bg),
                                 rendered_images=np32(preds["rendered_images"]), objective=np32(preds["objective"]))
 

@@ -1,0 +1,873 @@
+// NeRF MLP on gfx950: fused harmonic embedding + 8x256 trunk (skip) + heads, forward and backward.
+//
+// Reference: NeRFMLP (yanerf/pipelines/models/nerf_mlp.py:12-183), MLPWithInputSkips (:186-289),
+// HarmonicEmbedding / LinearWithRepeat (yanerf/pipelines/models/utils.py:17-211).
+//
+// Formulation: every layer is computed TRANSPOSED, out[feature n][point m] = sum_k W[n][k] act[m][k], so
+//   * A operand = weights, read straight from L2 in PyTorch's [out][in] layout (16 B per lane),
+//   * B operand = the point tile's activations, resident in LDS as point-major rows act[m][k],
+//   * the 16x16 accumulator holds 4 consecutive features of one point per lane, which is exactly one
+//     16-byte (fp32) / 8-byte (bf16) row segment of the next layer's LDS tile.
+// One workgroup owns a tile of M points for the whole network (PE -> 8 layers -> heads), so activations
+// never leave the CU between layers. Weights (1.19 MB bf16 / 2.4 MB fp32 per model) stream from the
+// XCD's L2. Both precisions use the same byte geometry: a K-block is 64 B of a row (16 fp32 = 4 x
+// v_mfma_f32_16x16x4_f32 with k permuted consistently on both operands, or 32 bf16 = 1 x
+// v_mfma_f32_16x16x32_bf16).
+//
+// LDS image: act[M][320] (cols 0..255 hidden, 256..319 xyz-PE / dir-PE), 16-byte chunks XOR-swizzled by
+// row so the 16 rows a ds_read_b128 lane group touches land on distinct bank slots.
+//
+// Backward: (1) a fused dX kernel walks the heads and trunk in reverse for a point tile, writing every
+// layer's pre-activation gradient dZ_l (feature-major, [row][point]); (2) a split-K dW kernel computes
+// dW_l = sum_points dZ_l x input_l (+ a virtual ones-row giving the bias gradient) into fp32 partial slabs,
+// (3) a deterministic reduce sums the slabs straight into the reference-layout parameter gradients.
+#include "common.hpp"
+
+namespace yanerf {
+
+typedef unsigned short bf16_t;
+
+template <typename T> struct Cfg;
+template <> struct Cfg<float> { static constexpr int M = 64, WAVES = 4, EPC = 4, KB = 16; };
+template <> struct Cfg<bf16_t> { static constexpr int M = 128, WAVES = 8, EPC = 8, KB = 32; };
+
+constexpr int ROW = 320;    // LDS row length (elements)
+constexpr int PE_COL = 256; // xyz-PE / dir-PE column base
+constexpr int KPE = 64;     // padded xyz PE width
+constexpr int KDIR = 32;    // padded dir PE width
+constexpr int KC = 288;     // color layer K (256 + 32)
+constexpr int HC = 128;     // padded color hidden width
+constexpr int CMAX = 4;
+constexpr int MAXL = 16;
+
+struct MlpLayout {
+  int L;
+  uint32_t skip;
+  int fx, fd, ax, ad, xyz_dim, dir_dim, hid, hdir, cdim;
+  int64_t w_off[MAXL];
+  int kpad[MAXL];
+  int64_t wt_off[MAXL];
+  int64_t wint_off, wintT_off, wc_off, wcT_off;
+  int64_t t_elems;
+  int64_t f_base;  // byte offset of the fp32 section
+  int64_t b_off[MAXL];
+  int64_t bint_off, bc_off, wd_off, bd_off, wo_off, bo_off;
+  int64_t f_elems;
+  int64_t bytes;
+};
+
+// saved activation rows (units of Npad elements of T)
+struct SavedRows {
+  int64_t pe, h0, y, dpe, c, rows;
+};
+__host__ __device__ inline SavedRows saved_rows(int L) {
+  SavedRows s;
+  s.pe = 0;
+  s.h0 = KPE;
+  s.y = s.h0 + 256LL * L;
+  s.dpe = s.y + 256;
+  s.c = s.dpe + KDIR;
+  s.rows = s.c + HC;
+  return s;
+}
+// backward gradient rows
+struct GradRows {
+  int64_t dz0, dyx, dzc, du, rows;
+};
+__host__ __device__ inline GradRows grad_rows(int L) {
+  GradRows g;
+  g.dz0 = 0;
+  g.dyx = 256LL * L;  // 256 rows dY + 1 row dsigma
+  g.dzc = g.dyx + 257;
+  g.du = g.dzc + HC;
+  g.rows = g.du + 16;
+  return g;
+}
+
+static int64_t tile_m(int prec) { return prec == YANERF_PREC_F32 ? Cfg<float>::M : Cfg<bf16_t>::M; }
+static int64_t npad_of(int prec, int64_t n) { int64_t M = tile_m(prec); return (n + M - 1) / M * M; }
+static size_t elem_size(int prec) { return prec == YANERF_PREC_F32 ? 4 : 2; }
+
+static int check_desc(const yanerf_mlp_desc* d) {
+  YN_CHECK(d, "mlp: null desc");
+  YN_CHECK(d->n_layers >= 1 && d->n_layers <= MAXL, "mlp: n_layers %d out of [1,%d]", d->n_layers, MAXL);
+  YN_CHECK((d->skip_mask & 1u) == 0, "mlp: a skip at layer 0 is not defined by the reference");
+  int xyz_dim = 3 * (2 * d->n_freq_xyz + (d->append_xyz ? 1 : 0));
+  int dir_dim = 3 * (2 * d->n_freq_dir + (d->append_dir ? 1 : 0));
+  YN_CHECK(d->n_freq_xyz >= 0 && xyz_dim <= KPE && xyz_dim > 0, "mlp: xyz embedding dim %d unsupported (<= %d)",
+           xyz_dim, KPE);
+  YN_CHECK(d->n_freq_dir >= 0 && dir_dim <= KDIR, "mlp: dir embedding dim %d unsupported (<= %d)", dir_dim, KDIR);
+  YN_CHECK(d->hidden_xyz >= 1 && d->hidden_xyz <= 256, "mlp: n_hidden_neurons_xyz %d unsupported", d->hidden_xyz);
+  YN_CHECK(d->hidden_dir >= 1 && d->hidden_dir <= HC, "mlp: n_hidden_neurons_dir %d unsupported", d->hidden_dir);
+  YN_CHECK(d->color_dim >= 1 && d->color_dim <= CMAX, "mlp: color_dim %d unsupported", d->color_dim);
+  return 0;
+}
+
+static MlpLayout make_layout(const yanerf_mlp_desc* d, int prec) {
+  MlpLayout L{};
+  L.L = d->n_layers;
+  L.skip = d->skip_mask;
+  L.fx = d->n_freq_xyz;
+  L.fd = d->n_freq_dir;
+  L.ax = d->append_xyz;
+  L.ad = d->append_dir;
+  L.xyz_dim = 3 * (2 * d->n_freq_xyz + (d->append_xyz ? 1 : 0));
+  L.dir_dim = 3 * (2 * d->n_freq_dir + (d->append_dir ? 1 : 0));
+  L.hid = d->hidden_xyz;
+  L.hdir = d->hidden_dir;
+  L.cdim = d->color_dim;
+  int64_t t = 0;
+  for (int l = 0; l < L.L; ++l) {
+    L.kpad[l] = (l == 0) ? KPE : ((L.skip >> l) & 1u) ? 320 : 256;
+    L.w_off[l] = t;
+    t += 256LL * L.kpad[l];
+  }
+  for (int l = 1; l < L.L; ++l) {
+    L.wt_off[l] = t;
+    t += 256LL * 256;
+  }
+  L.wint_off = t; t += 256LL * 256;
+  L.wintT_off = t; t += 256LL * 256;
+  L.wc_off = t; t += (int64_t)HC * KC;
+  L.wcT_off = t; t += 256LL * HC;
+  L.t_elems = t;
+  int64_t tb = t * (int64_t)elem_size(prec);
+  L.f_base = (tb + 255) / 256 * 256;
+  int64_t f = 0;
+  for (int l = 0; l < L.L; ++l) { L.b_off[l] = f; f += 256; }
+  L.bint_off = f; f += 256;
+  L.bc_off = f; f += HC;
+  L.wd_off = f; f += 256;
+  L.bd_off = f; f += 4;
+  L.wo_off = f; f += CMAX * HC;
+  L.bo_off = f; f += CMAX;
+  L.f_elems = f;
+  L.bytes = L.f_base + f * 4;
+  return L;
+}
+
+// ============================================================================================ pack
+struct PackJob {
+  const float* src;
+  int src_rows, src_ld;
+  int64_t dst_off;  // elements (T section) or floats (fp32 section)
+  int rows, cols;
+  int seg0, seg1_start, seg1_len;
+  int transpose, is_f32;
+  int64_t elem_base;
+};
+constexpr int kMaxPackJobs = 3 * MAXL + 12;
+struct PackJobs {
+  PackJob j[kMaxPackJobs];
+  int n;
+  int64_t total;
+};
+
+template <typename T>
+__global__ void pack_kernel(PackJobs jobs, T* __restrict__ dst_t, float* __restrict__ dst_f) {
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= jobs.total) return;
+  int lo = 0, hi = jobs.n - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (jobs.j[mid].elem_base <= e) lo = mid; else hi = mid - 1;
+  }
+  const PackJob& J = jobs.j[lo];
+  int64_t local = e - J.elem_base;
+  int r = (int)(local / J.cols), c = (int)(local % J.cols);
+  int n = J.transpose ? c : r;  // output-feature index
+  int k = J.transpose ? r : c;  // input-feature index (packed column)
+  int sk = -1;
+  if (k < J.seg0) sk = k;
+  else if (k >= J.seg1_start && k < J.seg1_start + J.seg1_len) sk = J.seg0 + (k - J.seg1_start);
+  float v = 0.0f;
+  if (sk >= 0 && n < J.src_rows) v = J.src[(int64_t)n * J.src_ld + sk];
+  if (J.is_f32) {
+    dst_f[J.dst_off + local] = v;
+  } else {
+    if constexpr (sizeof(T) == 4) dst_t[J.dst_off + local] = v;
+    else dst_t[J.dst_off + local] = f2bf(v);
+  }
+}
+
+// ============================================================================================ device core
+template <typename T> __device__ __forceinline__ int swz(int m, int c);
+template <> __device__ __forceinline__ int swz<float>(int m, int c) { return c ^ (m & 15); }
+template <> __device__ __forceinline__ int swz<bf16_t>(int m, int c) { return c ^ ((m >> 1) & 7); }
+
+template <typename T> __device__ __forceinline__ int lds_idx(int m, int col) {
+  constexpr int EPC = Cfg<T>::EPC;
+  return m * ROW + swz<T>(m, col / EPC) * EPC + (col % EPC);
+}
+template <typename T> __device__ __forceinline__ f4 lds_chunk(const T* act, int m, int c) {
+  return *(const f4*)(act + m * ROW + swz<T>(m, c) * Cfg<T>::EPC);
+}
+template <typename T> __device__ __forceinline__ T to_t(float v);
+template <> __device__ __forceinline__ float to_t<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16_t to_t<bf16_t>(float v) { return f2bf(v); }
+template <typename T> __device__ __forceinline__ float to_f(T v);
+template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f<bf16_t>(bf16_t v) { return bf2f(v); }
+
+template <typename T> __device__ __forceinline__ f4 mma_blk(f4 a, f4 b, f4 c);
+template <> __device__ __forceinline__ f4 mma_blk<float>(f4 a, f4 b, f4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
+  return c;
+}
+template <> __device__ __forceinline__ f4 mma_blk<bf16_t>(f4 a, f4 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a), __builtin_bit_cast(bf8, b), c, 0, 0, 0);
+}
+
+// acc[nt][mt] (rows nrow0 + 16nt.., points 16mt..) = W[rows][kblocks] x act[points][kblocks]^T
+template <typename T, int NT, int MT>
+__device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int nrow0, const T* act, int kc0, int nkb,
+                                         f4 (&acc)[NT][MT], int lane) {
+  constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
+  const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f4{0.f, 0.f, 0.f, 0.f};
+  const T* wp[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) wp[nt] = W + (size_t)(nrow0 + 16 * nt + li) * ldw + g * EPC;
+  f4 a[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) a[nt] = *(const f4*)(wp[nt]);
+  for (int kb = 0; kb < nkb; ++kb) {
+    f4 an[NT];
+    const int kn = (kb + 1 < nkb) ? kb + 1 : kb;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) an[nt] = *(const f4*)(wp[nt] + kn * KB);
+    f4 b[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) b[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + kb * 4 + g);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = mma_blk<T>(a[nt], b[mt], acc[nt][mt]);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) a[nt] = an[nt];
+  }
+}
+
+// write 4 consecutive features (rows n..n+3) of point m into the LDS tile
+template <typename T> __device__ __forceinline__ void lds_put4(T* act, int m, int n, f4 v);
+template <> __device__ __forceinline__ void lds_put4<float>(float* act, int m, int n, f4 v) {
+  *(f4*)(act + m * ROW + swz<float>(m, n / 4) * 4) = v;
+}
+template <> __device__ __forceinline__ void lds_put4<bf16_t>(bf16_t* act, int m, int n, f4 v) {
+  us4 h = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+  *(us4*)(act + m * ROW + swz<bf16_t>(m, n / 8) * 8 + (n & 7)) = h;
+}
+
+// harmonic embedding element k of 3-vector x (models/utils.py:98-102): [sin(x_i 2^f) i-major f-minor, cos, x]
+__device__ __forceinline__ float pe_value(const float x[3], int k, int F, int append) {
+  if (k < 3 * F) {
+    int i = k / F, f = k % F;
+    return sinf(x[i] * (float)(1 << f));
+  }
+  if (k < 6 * F) {
+    int kk = k - 3 * F;
+    int i = kk / F, f = kk % F;
+    return cosf(x[i] * (float)(1 << f));
+  }
+  if (append && k < 6 * F + 3) return x[k - 6 * F];
+  return 0.0f;
+}
+
+// ============================================================================================ forward
+template <typename T>
+__global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
+    MlpLayout lay, const T* __restrict__ Wt, const float* __restrict__ Wf, const float* __restrict__ origins,
+    const float* __restrict__ dirs, const float* __restrict__ lengths, int64_t R, int64_t P,
+    float* __restrict__ sigma, float* __restrict__ rgb, T* __restrict__ saved, int64_t Npad) {
+  constexpr int M = Cfg<T>::M, WAVES = Cfg<T>::WAVES, MT = M / 16;
+  constexpr int NT = 256 / 16 / WAVES, NTC = HC / 16 / WAVES;
+  constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
+  static_assert(M * 4 == WAVES * 64, "4 threads per point");
+  __shared__ __attribute__((aligned(16))) T act[M * ROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t N = R * P;
+  const int64_t p0 = (int64_t)blockIdx.x * M;
+  const SavedRows SR = saved_rows(lay.L);
+  const int mt_ = tid >> 2, q = tid & 3;
+  const int64_t p = p0 + mt_;
+  const int64_t pc = p < N ? p : N - 1;
+  const int64_t ray = pc / P;
+  float o3[3], d3[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    o3[i] = origins[ray * 3 + i];
+    d3[i] = dirs[ray * 3 + i];
+  }
+  const float t = lengths[pc];
+  float x3[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) x3[i] = o3[i] + t * d3[i];  // models/utils.py:244
+  for (int k = 16 * q; k < 16 * q + 16; ++k) {
+    float v = (k < lay.xyz_dim) ? pe_value(x3, k, lay.fx, lay.ax) : 0.0f;
+    act[lds_idx<T>(mt_, PE_COL + k)] = to_t<T>(v);
+    if (saved) saved[(SR.pe + k) * Npad + p] = to_t<T>(v);
+  }
+  __syncthreads();
+
+  f4 acc[NT][MT];
+  const int nrow0 = wave * NT * 16;
+  for (int l = 0; l < lay.L; ++l) {
+    const bool sk = (lay.skip >> l) & 1u;
+    const int kc0 = (l == 0) ? PE_COL / EPC : 0;
+    const int nkb = (l == 0) ? KPE / KB : (sk ? 320 / KB : 256 / KB);
+    gemm_lds<T, NT, MT>(Wt + lay.w_off[l], lay.kpad[l], nrow0, act, kc0, nkb, acc, lane);
+    __syncthreads();
+    const float* bias = Wf + lay.b_off[l];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = nrow0 + 16 * nt + 4 * g;
+      const f4 bv = *(const f4*)(bias + n);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        f4 v = acc[nt][mt] + bv;
+        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        const int m = 16 * mt + li;
+        lds_put4<T>(act, m, n, v);
+        if (saved) {
+          T* s = saved + (SR.h0 + 256LL * l + n) * Npad + p0 + m;
+          s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ---- density head (VALU): sigma = w_d . h + b_d  (nerf_mlp.py:173; density_layer 256->1)
+  float sig;
+  {
+    const float* wd = Wf + lay.wd_off;
+    float s = 0.0f;
+    for (int k = 64 * q; k < 64 * q + 64; ++k) s += wd[k] * to_f<T>(act[lds_idx<T>(mt_, k)]);
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    sig = s + Wf[lay.bd_off];
+  }
+  // ---- intermediate_linear (no activation)
+  gemm_lds<T, NT, MT>(Wt + lay.wint_off, 256, nrow0, act, 0, 256 / KB, acc, lane);
+  __syncthreads();
+  {
+    const float* bias = Wf + lay.bint_off;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = nrow0 + 16 * nt + 4 * g;
+      const f4 bv = *(const f4*)(bias + n);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        f4 v = acc[nt][mt] + bv;
+        const int m = 16 * mt + li;
+        lds_put4<T>(act, m, n, v);
+        if (saved) {
+          T* s = saved + (SR.y + n) * Npad + p0 + m;
+          s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
+        }
+      }
+    }
+  }
+  // ---- direction embedding of normalize(d) (nerf_mlp.py:105-108) into cols 256..287
+  {
+    const float nrm = fmaxf(sqrtf(d3[0] * d3[0] + d3[1] * d3[1] + d3[2] * d3[2]), 1e-12f);
+    float dn[3] = {d3[0] / nrm, d3[1] / nrm, d3[2] / nrm};
+    for (int k = 8 * q; k < 8 * q + 8; ++k) {
+      float v = (k < lay.dir_dim) ? pe_value(dn, k, lay.fd, lay.ad) : 0.0f;
+      act[lds_idx<T>(mt_, PE_COL + k)] = to_t<T>(v);
+      if (saved) saved[(SR.dpe + k) * Npad + p] = to_t<T>(v);
+    }
+  }
+  __syncthreads();
+  // ---- color layer: LinearWithRepeat(256 + 27 -> 128) + ReLU as one K = 288 GEMM over [Y, dirPE]
+  {
+    f4 accc[NTC][MT];
+    const int crow0 = wave * NTC * 16;
+    gemm_lds<T, NTC, MT>(Wt + lay.wc_off, KC, crow0, act, 0, KC / KB, accc, lane);
+    __syncthreads();
+    const float* bias = Wf + lay.bc_off;
+#pragma unroll
+    for (int nt = 0; nt < NTC; ++nt) {
+      const int n = crow0 + 16 * nt + 4 * g;
+      const f4 bv = *(const f4*)(bias + n);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        f4 v = accc[nt][mt] + bv;
+        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        const int m = 16 * mt + li;
+        lds_put4<T>(act, m, n, v);
+        if (saved) {
+          T* s = saved + (SR.c + n) * Npad + p0 + m;
+          s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- output layer 128 -> color_dim + sigmoid (VALU)
+  {
+    const float* wo = Wf + lay.wo_off;
+    float u[CMAX] = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 32 * q; c < 32 * q + 32; ++c) {
+      float cv = to_f<T>(act[lds_idx<T>(mt_, c)]);
+#pragma unroll
+      for (int j = 0; j < CMAX; ++j) u[j] += wo[j * HC + c] * cv;
+    }
+#pragma unroll
+    for (int j = 0; j < CMAX; ++j) {
+      u[j] += __shfl_xor(u[j], 1, 64);
+      u[j] += __shfl_xor(u[j], 2, 64);
+    }
+    if (q == 0 && p < N) {
+      sigma[p] = sig;
+      for (int j = 0; j < lay.cdim; ++j) {
+        float z = u[j] + Wf[lay.bo_off + j];
+        rgb[p * lay.cdim + j] = 1.0f / (1.0f + expf(-z));
+      }
+    }
+  }
+}
+
+// ============================================================================================ backward dX
+template <typename T>
+__global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
+    MlpLayout lay, const T* __restrict__ Wt, const float* __restrict__ Wf, const T* __restrict__ saved,
+    const float* __restrict__ rgb, const float* __restrict__ g_sigma, const float* __restrict__ g_rgb, int64_t N,
+    int64_t Npad, T* __restrict__ grad) {
+  constexpr int M = Cfg<T>::M, WAVES = Cfg<T>::WAVES, MT = M / 16;
+  constexpr int NT = 256 / 16 / WAVES;
+  constexpr int KB = Cfg<T>::KB;
+  __shared__ __attribute__((aligned(16))) T act[M * ROW];
+  __shared__ float s_gs[M];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t p0 = (int64_t)blockIdx.x * M;
+  const SavedRows SR = saved_rows(lay.L);
+  const GradRows GR = grad_rows(lay.L);
+  const int mt_ = tid >> 2, q = tid & 3;
+  const int64_t p = p0 + mt_;
+  const bool valid = p < N;
+  const int cd = lay.cdim;
+  // ---- sigmoid backward (grad * (1 - y) * y) and output layer backward
+  float du[CMAX] = {0.f, 0.f, 0.f, 0.f};
+  const float gs = valid ? g_sigma[p] : 0.0f;
+  for (int j = 0; j < cd; ++j) {
+    if (valid) {
+      float y = rgb[p * cd + j];
+      du[j] = (g_rgb[p * cd + j] * (1.0f - y)) * y;
+    }
+  }
+  if (q == 0) {
+    for (int j = 0; j < cd; ++j) grad[(GR.du + j) * Npad + p] = to_t<T>(du[j]);
+    grad[(GR.dyx + 256) * Npad + p] = to_t<T>(gs);
+    s_gs[mt_] = gs;
+  }
+  {
+    const float* wo = Wf + lay.wo_off;
+    for (int c = 32 * q; c < 32 * q + 32; ++c) {
+      float dc = 0.0f;
+      for (int j = 0; j < cd; ++j) dc += du[j] * wo[j * HC + c];
+      float cval = to_f<T>(saved[(SR.c + c) * Npad + p]);
+      float dz = cval > 0.0f ? dc : 0.0f;
+      act[lds_idx<T>(mt_, c)] = to_t<T>(dz);
+      grad[(GR.dzc + c) * Npad + p] = to_t<T>(dz);
+    }
+  }
+  __syncthreads();
+  f4 acc[NT][MT];
+  const int nrow0 = wave * NT * 16;
+  // ---- dY = Wc[:, :256]^T dZc   (K = 128)
+  gemm_lds<T, NT, MT>(Wt + lay.wcT_off, HC, nrow0, act, 0, HC / KB, acc, lane);
+  __syncthreads();
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int n = nrow0 + 16 * nt + 4 * g;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = 16 * mt + li;
+      f4 v = acc[nt][mt];
+      lds_put4<T>(act, m, n, v);
+      T* s = grad + (GR.dyx + n) * Npad + p0 + m;
+      s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
+    }
+  }
+  __syncthreads();
+  // ---- dH_{L-1} = Wint^T dY + w_d (x) dsigma ; dZ_{L-1} = dH * [H_{L-1} > 0]
+  for (int l = lay.L; l >= 1; --l) {
+    // l == L: the heads -> last trunk layer; else trunk layer l -> layer l-1
+    const T* A = (l == lay.L) ? Wt + lay.wintT_off : Wt + lay.wt_off[l];
+    const int hl = l - 1;  // layer whose output gradient we form
+    // prefetch relu masks of H_{hl}
+    f4 hm[NT][MT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int n = nrow0 + 16 * nt + 4 * g, m = 16 * mt + li;
+        const T* s = saved + (SR.h0 + 256LL * hl + n) * Npad + p0 + m;
+        hm[nt][mt] = f4{to_f<T>(s[0]), to_f<T>(s[Npad]), to_f<T>(s[2 * Npad]), to_f<T>(s[3 * Npad])};
+      }
+    gemm_lds<T, NT, MT>(A, 256, nrow0, act, 0, 256 / KB, acc, lane);
+    __syncthreads();
+    const float* wd = Wf + lay.wd_off;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = nrow0 + 16 * nt + 4 * g;
+      f4 wdv = (l == lay.L) ? *(const f4*)(wd + n) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = 16 * mt + li;
+        f4 v = acc[nt][mt];
+        if (l == lay.L) v = v + wdv * s_gs[m];
+        v.x = hm[nt][mt].x > 0.f ? v.x : 0.f;
+        v.y = hm[nt][mt].y > 0.f ? v.y : 0.f;
+        v.z = hm[nt][mt].z > 0.f ? v.z : 0.f;
+        v.w = hm[nt][mt].w > 0.f ? v.w : 0.f;
+        lds_put4<T>(act, m, n, v);
+        T* s = grad + (GR.dz0 + 256LL * hl + n) * Npad + p0 + m;
+        s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ============================================================================================ backward dW
+struct DwJob {
+  const void* A;
+  int a_rows;
+  const void* X0;
+  int x0_rows;
+  const void* X1;
+  int x1_rows;
+  int kv;  // x0 + x1 + 1 (ones row -> bias)
+  int n_tiles, k_tiles, tile_base;
+  int64_t slab_off;
+  float* W0;
+  float* b0;
+  int r0_begin, r0_count;
+  float* W1;
+  float* b1;
+  int r1_begin, r1_count;
+};
+constexpr int kMaxDwJobs = MAXL + 3;
+struct DwJobs {
+  DwJob j[kMaxDwJobs];
+  int n;
+  int total_tiles;
+  int64_t slab_elems;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) mlp_dw_kernel(DwJobs jobs, int64_t Npad, int S, float* __restrict__ slab) {
+  constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
+  const int tile = blockIdx.x, s = blockIdx.y;
+  int ji = 0;
+  while (ji + 1 < jobs.n && jobs.j[ji + 1].tile_base <= tile) ++ji;
+  const DwJob& J = jobs.j[ji];
+  const int lt = tile - J.tile_base;
+  const int n0 = (lt / J.k_tiles) * 64, k0 = (lt % J.k_tiles) * 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int64_t nblk = Npad / KB;
+  const int64_t b_lo = nblk * s / S, b_hi = nblk * (s + 1) / S;
+  const int an = n0 + 16 * wave + li;
+  const T* arow = (an < J.a_rows) ? (const T*)J.A + (int64_t)an * Npad : nullptr;
+  const T* xrow[4];
+  bool ones[4];
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    const int k = k0 + 16 * kt + li;
+    xrow[kt] = nullptr;
+    ones[kt] = false;
+    if (k < J.x0_rows) xrow[kt] = (const T*)J.X0 + (int64_t)k * Npad;
+    else if (k < J.x0_rows + J.x1_rows) xrow[kt] = (const T*)J.X1 + (int64_t)(k - J.x0_rows) * Npad;
+    else if (k == J.kv - 1) ones[kt] = true;
+  }
+  f4 onev;
+  if constexpr (sizeof(T) == 4) onev = f4{1.f, 1.f, 1.f, 1.f};
+  else onev = __builtin_bit_cast(f4, us8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80});
+  const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
+  f4 acc[4] = {zero, zero, zero, zero};
+  for (int64_t blk = b_lo; blk < b_hi; ++blk) {
+    const int64_t pb = blk * KB + g * EPC;
+    f4 a = arow ? *(const f4*)(arow + pb) : zero;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      f4 b = xrow[kt] ? *(const f4*)(xrow[kt] + pb) : (ones[kt] ? onev : zero);
+      acc[kt] = mma_blk<T>(a, b, acc[kt]);
+    }
+  }
+  float* out = slab + (int64_t)s * jobs.slab_elems + J.slab_off;
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    const int k = k0 + 16 * kt + li;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + 16 * wave + 4 * g + r;
+      if (n < J.a_rows && k < J.kv) out[(int64_t)n * J.kv + k] = acc[kt][r];
+    }
+  }
+}
+
+__global__ void dw_reduce_kernel(DwJobs jobs, int S, const float* __restrict__ slab) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= jobs.slab_elems) return;
+  int ji = 0;
+  while (ji + 1 < jobs.n && jobs.j[ji + 1].slab_off <= e) ++ji;
+  const DwJob& J = jobs.j[ji];
+  const int64_t local = e - J.slab_off;
+  const int n = (int)(local / J.kv), k = (int)(local % J.kv);
+  float sum = 0.0f;
+  for (int s = 0; s < S; ++s) sum += slab[(int64_t)s * jobs.slab_elems + e];
+  const int ktot = J.kv - 1;
+  if (n >= J.r0_begin && n < J.r0_begin + J.r0_count) {
+    if (k < ktot) J.W0[(int64_t)(n - J.r0_begin) * ktot + k] = sum;
+    else J.b0[n - J.r0_begin] = sum;
+  } else if (J.W1 && n >= J.r1_begin && n < J.r1_begin + J.r1_count) {
+    if (k < ktot) J.W1[(int64_t)(n - J.r1_begin) * ktot + k] = sum;
+    else J.b1[n - J.r1_begin] = sum;
+  }
+}
+
+// ============================================================================================ host helpers
+static int num_params(const yanerf_mlp_desc* d) { return 2 * d->n_layers + 8; }
+
+static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, const float* const* prm, PackJobs& J) {
+  J.n = 0;
+  J.total = 0;
+  auto add = [&](const float* src, int src_rows, int src_ld, int64_t dst_off, int rows, int cols, int seg0,
+                 int seg1_start, int seg1_len, int transpose, int is_f32) {
+    PackJob& j = J.j[J.n++];
+    j.src = src; j.src_rows = src_rows; j.src_ld = src_ld; j.dst_off = dst_off; j.rows = rows; j.cols = cols;
+    j.seg0 = seg0; j.seg1_start = seg1_start; j.seg1_len = seg1_len; j.transpose = transpose; j.is_f32 = is_f32;
+    j.elem_base = J.total;
+    J.total += (int64_t)rows * cols;
+  };
+  const int nl = L.L;
+  for (int l = 0; l < nl; ++l) {
+    const float* W = prm[2 * l];
+    const float* b = prm[2 * l + 1];
+    const int nout = (l + 1 < nl) ? 256 : L.hid;
+    const bool sk = (L.skip >> l) & 1u;
+    const int src_ld = (l == 0) ? L.xyz_dim : (sk ? 256 + L.xyz_dim : 256);
+    if (l == 0) add(W, nout, src_ld, L.w_off[0], 256, KPE, L.xyz_dim, 0, 0, 0, 0);
+    else if (sk) add(W, nout, src_ld, L.w_off[l], 256, 320, 256, 256, L.xyz_dim, 0, 0);
+    else add(W, nout, src_ld, L.w_off[l], 256, 256, 256, 0, 0, 0, 0);
+    if (l >= 1) add(W, nout, src_ld, L.wt_off[l], 256, 256, 256, 0, 0, 1, 0);
+    add(b, 1, nout, L.b_off[l], 1, 256, nout, 0, 0, 0, 1);
+  }
+  const float** h = (const float**)prm + 2 * nl;
+  // intermediate_linear [hid][hid], density [1][hid], color0 [hd][hid + dir], color2 [cd][hd]
+  add(h[0], L.hid, L.hid, L.wint_off, 256, 256, L.hid, 0, 0, 0, 0);
+  add(h[0], L.hid, L.hid, L.wintT_off, 256, 256, L.hid, 0, 0, 1, 0);
+  add(h[1], 1, L.hid, L.bint_off, 1, 256, L.hid, 0, 0, 0, 1);
+  add(h[2], 1, L.hid, L.wd_off, 1, 256, L.hid, 0, 0, 0, 1);
+  add(h[3], 1, 1, L.bd_off, 1, 4, 1, 0, 0, 0, 1);
+  add(h[4], L.hdir, L.hid + L.dir_dim, L.wc_off, HC, KC, L.hid, 256, L.dir_dim, 0, 0);
+  add(h[4], L.hdir, L.hid + L.dir_dim, L.wcT_off, 256, HC, L.hid, 0, 0, 1, 0);
+  add(h[5], 1, L.hdir, L.bc_off, 1, HC, L.hdir, 0, 0, 0, 1);
+  add(h[6], L.cdim, L.hdir, L.wo_off, CMAX, HC, L.hdir, 0, 0, 0, 1);
+  add(h[7], 1, L.cdim, L.bo_off, 1, CMAX, L.cdim, 0, 0, 0, 1);
+  return 0;
+}
+
+static int dw_splits(int total_tiles, int64_t nblk) {
+  int64_t S = (2048 + total_tiles - 1) / total_tiles;
+  if (S > nblk) S = nblk;
+  if (S > 64) S = 64;
+  if (S < 1) S = 1;
+  return (int)S;
+}
+
+static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void* gradbuf, int64_t Npad,
+                          float* const* grads, DwJobs& D) {
+  const size_t es = elem_size(prec);
+  const SavedRows SR = saved_rows(L.L);
+  const GradRows GR = grad_rows(L.L);
+  auto srow = [&](int64_t r) { return (const void*)((const char*)saved + r * Npad * es); };
+  auto grow = [&](int64_t r) { return (const void*)((const char*)gradbuf + r * Npad * es); };
+  D.n = 0;
+  D.total_tiles = 0;
+  D.slab_elems = 0;
+  auto add = [&](const void* A, int a_rows, const void* X0, int x0, const void* X1, int x1, float* W0, float* b0,
+                 int r0b, int r0c, float* W1, float* b1, int r1b, int r1c) {
+    DwJob& j = D.j[D.n++];
+    j.A = A; j.a_rows = a_rows; j.X0 = X0; j.x0_rows = x0; j.X1 = X1; j.x1_rows = x1;
+    j.kv = x0 + x1 + 1;
+    j.n_tiles = (a_rows + 63) / 64;
+    j.k_tiles = (j.kv + 63) / 64;
+    j.tile_base = D.total_tiles;
+    D.total_tiles += j.n_tiles * j.k_tiles;
+    j.slab_off = D.slab_elems;
+    D.slab_elems += (int64_t)a_rows * j.kv;
+    j.W0 = W0; j.b0 = b0; j.r0_begin = r0b; j.r0_count = r0c;
+    j.W1 = W1; j.b1 = b1; j.r1_begin = r1b; j.r1_count = r1c;
+  };
+  for (int l = 0; l < L.L; ++l) {
+    const int nout = (l + 1 < L.L) ? 256 : L.hid;
+    const bool sk = (L.skip >> l) & 1u;
+    const void* A = grow(GR.dz0 + 256LL * l);
+    if (l == 0) add(A, nout, srow(SR.pe), L.xyz_dim, nullptr, 0, grads[0], grads[1], 0, nout, nullptr, nullptr, 0, 0);
+    else if (sk)
+      add(A, nout, srow(SR.h0 + 256LL * (l - 1)), 256, srow(SR.pe), L.xyz_dim, grads[2 * l], grads[2 * l + 1], 0, nout,
+          nullptr, nullptr, 0, 0);
+    else
+      add(A, nout, srow(SR.h0 + 256LL * (l - 1)), 256, nullptr, 0, grads[2 * l], grads[2 * l + 1], 0, nout, nullptr,
+          nullptr, 0, 0);
+  }
+  float* const* h = grads + 2 * L.L;
+  add(grow(GR.dyx), 257, srow(SR.h0 + 256LL * (L.L - 1)), L.hid, nullptr, 0, h[0], h[1], 0, L.hid, h[2], h[3], 256, 1);
+  add(grow(GR.dzc), L.hdir, srow(SR.y), L.hid, srow(SR.dpe), L.dir_dim, h[4], h[5], 0, L.hdir, nullptr, nullptr, 0, 0);
+  add(grow(GR.du), L.cdim, srow(SR.c), L.hdir, nullptr, 0, h[6], h[7], 0, L.cdim, nullptr, nullptr, 0, 0);
+}
+
+static int64_t dw_slab_elems_for(const MlpLayout& L, int* total_tiles) {
+  // mirror of build_dw_jobs' sizes
+  int64_t e = 0;
+  int tiles = 0;
+  auto acc = [&](int a_rows, int kin) {
+    int kv = kin + 1;
+    e += (int64_t)a_rows * kv;
+    tiles += ((a_rows + 63) / 64) * ((kv + 63) / 64);
+  };
+  for (int l = 0; l < L.L; ++l) {
+    const int nout = (l + 1 < L.L) ? 256 : L.hid;
+    const bool sk = (L.skip >> l) & 1u;
+    acc(nout, l == 0 ? L.xyz_dim : (sk ? 256 + L.xyz_dim : 256));
+  }
+  acc(257, L.hid);
+  acc(L.hdir, L.hid + L.dir_dim);
+  acc(L.cdim, L.hdir);
+  if (total_tiles) *total_tiles = tiles;
+  return e;
+}
+
+template <typename T>
+static int launch_fwd(const MlpLayout& L, const void* packed, const float* o, const float* d, const float* t, int64_t R,
+                      int64_t P, float* sigma, float* rgb, void* saved, hipStream_t st) {
+  const int64_t N = R * P;
+  const int64_t Npad = npad_of(sizeof(T) == 4 ? YANERF_PREC_F32 : YANERF_PREC_BF16, N);
+  const T* Wt = (const T*)packed;
+  const float* Wf = (const float*)((const char*)packed + L.f_base);
+  dim3 grid((unsigned)(Npad / Cfg<T>::M)), block(Cfg<T>::WAVES * 64);
+  hipLaunchKernelGGL(mlp_fwd_kernel<T>, grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, (T*)saved, Npad);
+  YN_LAUNCH_CHECK("mlp_forward");
+  return 0;
+}
+
+template <typename T>
+static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const void* saved, const float* rgb,
+                      const float* gs, const float* gr, int64_t N, float* const* grads, void* ws, hipStream_t st) {
+  const int64_t Npad = npad_of(prec, N);
+  const T* Wt = (const T*)packed;
+  const float* Wf = (const float*)((const char*)packed + L.f_base);
+  const GradRows GR = grad_rows(L.L);
+  T* gradbuf = (T*)ws;
+  int64_t grad_bytes = (GR.rows * Npad * (int64_t)sizeof(T) + 255) / 256 * 256;
+  float* slab = (float*)((char*)ws + grad_bytes);
+  hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::WAVES * 64), 0, st, L, Wt,
+                     Wf, (const T*)saved, rgb, gs, gr, N, Npad, gradbuf);
+  YN_LAUNCH_CHECK("mlp_backward_dx");
+  DwJobs D;
+  build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D);
+  const int S = dw_splits(D.total_tiles, Npad / Cfg<T>::KB);
+  hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)D.total_tiles, (unsigned)S), dim3(256), 0, st, D, Npad, S, slab);
+  YN_LAUNCH_CHECK("mlp_backward_dw");
+  hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((D.slab_elems + 255) / 256)), dim3(256), 0, st, D, S, slab);
+  YN_LAUNCH_CHECK("mlp_backward_reduce");
+  return 0;
+}
+
+}  // namespace yanerf
+
+using namespace yanerf;
+
+extern "C" {
+
+int yanerf_mlp_num_params(const yanerf_mlp_desc* d) {
+  if (check_desc(d)) return -1;
+  return num_params(d);
+}
+
+int64_t yanerf_mlp_packed_bytes(const yanerf_mlp_desc* d, int precision) {
+  if (check_desc(d)) return -1;
+  return make_layout(d, precision).bytes;
+}
+
+int yanerf_mlp_pack(const yanerf_mlp_desc* d, int precision, const float* const* params, void* packed, void* stream) {
+  if (check_desc(d)) return 1;
+  YN_CHECK(precision == YANERF_PREC_F32 || precision == YANERF_PREC_BF16, "mlp_pack: bad precision %d", precision);
+  YN_CHECK(params && packed, "mlp_pack: null pointer");
+  for (int i = 0; i < num_params(d); ++i) YN_CHECK(params[i], "mlp_pack: parameter %d is null", i);
+  MlpLayout L = make_layout(d, precision);
+  PackJobs J;
+  build_pack_jobs(d, L, params, J);
+  char* base = (char*)packed;
+  float* fsec = (float*)(base + L.f_base);
+  dim3 grid((unsigned)((J.total + 255) / 256)), block(256);
+  if (precision == YANERF_PREC_F32)
+    hipLaunchKernelGGL(pack_kernel<float>, grid, block, 0, as_stream(stream), J, (float*)base, fsec);
+  else
+    hipLaunchKernelGGL(pack_kernel<bf16_t>, grid, block, 0, as_stream(stream), J, (bf16_t*)base, fsec);
+  YN_LAUNCH_CHECK("mlp_pack");
+  return 0;
+}
+
+int64_t yanerf_mlp_saved_bytes(const yanerf_mlp_desc* d, int precision, int64_t n_points) {
+  if (check_desc(d)) return -1;
+  return saved_rows(d->n_layers).rows * npad_of(precision, n_points) * (int64_t)elem_size(precision);
+}
+
+int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, int64_t n_points) {
+  if (check_desc(d)) return -1;
+  MlpLayout L = make_layout(d, precision);
+  const int64_t Npad = npad_of(precision, n_points);
+  const GradRows GR = grad_rows(d->n_layers);
+  int64_t grad_bytes = (GR.rows * Npad * (int64_t)elem_size(precision) + 255) / 256 * 256;
+  int tiles = 0;
+  int64_t se = dw_slab_elems_for(L, &tiles);
+  const int64_t kb = precision == YANERF_PREC_F32 ? Cfg<float>::KB : Cfg<bf16_t>::KB;
+  int S = dw_splits(tiles, Npad / kb);
+  return grad_bytes + (int64_t)S * se * 4;
+}
+
+int yanerf_mlp_forward(const yanerf_mlp_desc* d, int precision, const void* packed, const float* origins,
+                       const float* directions, const float* lengths, int64_t R, int64_t P, float* sigma_raw,
+                       float* rgb, void* saved, void* stream) {
+  if (check_desc(d)) return 1;
+  YN_CHECK(packed && origins && directions && lengths && sigma_raw && rgb, "mlp_forward: null pointer");
+  YN_CHECK(R >= 0 && P >= 1, "mlp_forward: bad sizes R=%lld P=%lld", (long long)R, (long long)P);
+  if (R == 0) return 0;
+  MlpLayout L = make_layout(d, precision);
+  if (precision == YANERF_PREC_F32)
+    return launch_fwd<float>(L, packed, origins, directions, lengths, R, P, sigma_raw, rgb, saved, as_stream(stream));
+  if (precision == YANERF_PREC_BF16)
+    return launch_fwd<bf16_t>(L, packed, origins, directions, lengths, R, P, sigma_raw, rgb, saved, as_stream(stream));
+  YN_CHECK(false, "mlp_forward: bad precision %d", precision);
+}
+
+int yanerf_mlp_backward(const yanerf_mlp_desc* d, int precision, const void* packed, const void* saved,
+                        const float* rgb, const float* g_sigma, const float* g_rgb, int64_t R, int64_t P,
+                        float* const* grads, void* workspace, void* stream) {
+  if (check_desc(d)) return 1;
+  YN_CHECK(packed && saved && rgb && g_sigma && g_rgb && grads && workspace, "mlp_backward: null pointer");
+  for (int i = 0; i < num_params(d); ++i) YN_CHECK(grads[i], "mlp_backward: grad %d is null", i);
+  if (R * P == 0) return 0;
+  MlpLayout L = make_layout(d, precision);
+  if (precision == YANERF_PREC_F32)
+    return launch_bwd<float>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R * P, grads, workspace,
+                             as_stream(stream));
+  if (precision == YANERF_PREC_BF16)
+    return launch_bwd<bf16_t>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R * P, grads, workspace,
+                              as_stream(stream));
+  YN_CHECK(false, "mlp_backward: bad precision %d", precision);
+}
+
+}  // extern "C"

@@ -1,0 +1,222 @@
+#!/usr/bin/env python
+"""Benchmark: NeRF training-step throughput (rays/s) on Lego 800x800, 64 coarse + 128 fine samples
+(BASELINE.json configs[1]; configs[2] at N GPUs), MI355X HIP path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32|bf16] [--rays 4096]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+A step = one rank's training step on one synthetic 800x800 image (4096 rays, 64 + (64+128) points per ray):
+raygen -> coarse MLP -> composite -> refine -> fine MLP -> composite -> loss -> backward (both MLPs) ->
+RCCL gradient all-reduce -> Adam. Inputs (target image, poses) are resident in HBM before timing; weights are
+random-init of the Lego architecture; targets are synthetic (no dataset in this environment). Weak scaling:
+every rank runs its own 4096-ray step, value = total rays of all ranks / max-over-ranks time.
+
+Rank 0 prints ONE JSON line (contract in the task statement), with `roofline` for the dominant kernel
+(fine-pass fused MLP forward, timed with HIP events on the launch stream) and `cpu_baseline` (the CPU oracle's
+training step on a bounded sample, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import yanerf_boot  # noqa: E402,F401
+from yanerf_amd import parallel  # noqa: E402
+from yanerf_amd.train import NeRFTrainer  # noqa: E402
+from yanerf_amd.utils.config import Config  # noqa: E402
+
+METRIC = "rays/sec (train step) + PSNR, Lego 800×800 64c+128f, 1/2/4/8 MI355X"
+MAC_PER_POINT = 589_952  # 63*256 + 4*256^2 + 319*256 + 2*256^2 + 256^2 + 256 + 256*128 + 128*3
+MAC_PER_RAY_PASS = 27 * 128  # LinearWithRepeat direction term, once per ray per pass
+PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}  # MI355X dense matrix peaks (MI355X_MICROARCH.md)
+
+
+def synthetic_pose(theta, phi, radius=4.0):
+    """Camera on a sphere, Blender c2w convention + the reference's flip diag(1,-1,-1,1)
+    (blender_dataset.py:58-60, 69)."""
+    def tr(t):
+        return np.array([[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 1, t], [0, 0, 0, 1]], np.float64)
+
+    def rphi(p):
+        c, s = math.cos(p), math.sin(p)
+        return np.array([[1, 0, 0, 0], [0, c, -s, 0], [0, s, c, 0], [0, 0, 0, 1]], np.float64)
+
+    def rth(t):
+        c, s = math.cos(t), math.sin(t)
+        return np.array([[c, 0, -s, 0], [0, 1, 0, 0], [s, 0, c, 0], [0, 0, 0, 1]], np.float64)
+
+    c2w = rth(math.radians(theta)) @ rphi(math.radians(phi)) @ tr(radius)
+    c2w = np.array([[-1, 0, 0, 0], [0, 0, 1, 0], [0, 1, 0, 0], [0, 0, 0, 1]], np.float64) @ c2w
+    return (c2w @ np.diag([1.0, -1.0, -1.0, 1.0]))[:3, :4].astype(np.float32)
+
+
+def train_flops_per_ray(pc: int, pf: int) -> float:
+    fwd = 2.0 * (MAC_PER_POINT * (pc + pf) + 2 * MAC_PER_RAY_PASS)
+    return 3.0 * fwd  # forward + input-gradient chain + weight gradients
+
+
+def cpu_baseline(precision_cfg, n_pts_c: int, n_pts_f_new: int, budget_s: float = 12.0):
+    """The CPU oracle (numpy restatement, tests' checker) timed on a bounded sample of the same workload."""
+    sys.path.insert(0, str(ROOT / "tests" / "golden"))
+    from oracle import nerf_oracle as O  # noqa: E402  (cpu_baseline leg only)
+    from weights import LEGO_ARCH, make_nerf_mlp_params  # noqa: E402
+    threads = int(os.environ.get("YANERF_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    try:
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(threads)
+    except Exception:  # pragma: no cover
+        limiter = None
+    arch = O.MLPArch.from_dict(LEGO_ARCH)
+    pc, pf = make_nerf_mlp_params(LEGO_ARCH, 1), make_nerf_mlp_params(LEGO_ARCH, 2)
+    cfg = O.RenderCfg(n_pts_coarse=n_pts_c, n_pts_fine=n_pts_f_new, density_noise_std=0.2,
+                      raymarch=O.RaymarchOpts(background_density_bias=1e-6))
+    rng = np.random.default_rng(0)
+    R = 256
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        o = np.tile([[0.0, 0.0, 4.0]], (R, 1)).astype(np.float32)
+        d = (rng.standard_normal((R, 3)) * 0.3 + [0, 0, -1]).astype(np.float32)
+        z = O.jiggle_within_stratas(np.broadcast_to(O.torch_linspace(2, 6, n_pts_c), (R, n_pts_c)).copy(),
+                                    rng.random((R, n_pts_c)).astype(np.float32))
+        O.train_step_grads(pc, pf, arch, cfg, o, d, z, rng.random((R, 3)).astype(np.float32),
+                           (rng.standard_normal((R, n_pts_c)) * 0.2).astype(np.float32),
+                           (rng.standard_normal((R, n_pts_c + n_pts_f_new)) * 0.2).astype(np.float32),
+                           rng.random((R, n_pts_f_new)).astype(np.float32))
+        done += R
+    dt = time.perf_counter() - t0
+    if limiter is not None:
+        limiter.unregister()
+    return {"value": round(done / dt, 2), "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"{done} rays of the Lego 64+{n_pts_f_new} training step (fwd+bwd both MLPs, no optimizer) "
+                      f"in batches of {R}, numpy fp32 oracle, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--precision", default=os.environ.get("YANERF_BENCH_PRECISION", "fp32"), choices=["fp32", "bf16"])
+    ap.add_argument("--rays", type=int, default=None, help="rays per rank per step (default: config, 4096)")
+    ap.add_argument("--config", default=str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml"))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--secondary", default="bf16", help="also time this precision (reported under `secondary`)")
+    args = ap.parse_args()
+
+    rank, world, local = parallel.init_distributed()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    cfg = Config.fromfile(args.config)
+    pcfg = cfg.pipeline
+    H, W = int(pcfg.ray_sampler.image_height), int(pcfg.ray_sampler.image_width)
+    focal_px = 0.5 * W / math.tan(0.5 * 0.6911112)  # nerf_synthetic camera_angle_x
+    g = torch.Generator().manual_seed(42 + rank)  # seed + rank (run.py:70-73)
+    image = torch.rand(1, H, W, 3, generator=g).to(dev)
+    poses = torch.stack([torch.from_numpy(synthetic_pose(th, -30.0)) for th in np.linspace(-180, 180, 40,
+                                                                                            endpoint=False)]).to(dev)
+    focal = torch.tensor([focal_px], device=dev)
+
+    def run(precision: str, steps: int, warmup: int, probes: bool):
+        tr = NeRFTrainer(pcfg, precision=precision, device=dev, lr=float(cfg.runner.init_lr) * world,
+                         n_rays=args.rays)
+        for i in range(warmup):
+            tr.step(poses[(i + rank) % len(poses)][None], focal, image)
+        if probes:
+            tr.enable_probes(["mlp_fwd_0", "mlp_fwd_1", "mlp_bwd_0", "mlp_bwd_1"])
+        parallel.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = None
+        for i in range(steps):
+            out = tr.step(poses[(warmup + i + rank) % len(poses)][None], focal, image)
+        torch.cuda.synchronize()
+        parallel.barrier()
+        dt = parallel.max_over_ranks(time.perf_counter() - t0, device=dev)
+        mse_f = float(out["sq_fine"].mean().item() / 3.0)
+        return tr, dt, mse_f
+
+    tr, dt, mse_f = run(args.precision, args.steps, args.warmup, probes=True)
+    R, Pc, Pf = tr.R, tr.Pc, tr.Pf
+    rays_total = R * world * args.steps
+    value = rays_total / dt
+    ms_step = 1e3 * dt / args.steps
+    probe = tr.probe_ms()
+    flops_ray = train_flops_per_ray(Pc, Pf)
+    # roofline of the dominant kernel: fine-pass fused PE+MLP+heads forward (one launch per step)
+    fwd_flops = 2.0 * (MAC_PER_POINT * R * Pf + MAC_PER_RAY_PASS * R)
+    fwd_ms = probe.get("mlp_fwd_1", float("nan"))
+    achieved = fwd_flops / (fwd_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.precision]
+    pmc_file = ROOT / "profiles" / f"pmc_mlp_fwd_{args.precision}.json"
+    traffic = None
+    if pmc_file.exists():
+        try:
+            traffic = json.loads(pmc_file.read_text()).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    result = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if args.precision == "fp32" else "bf16",
+        "data": "synthetic (random 800x800 target per rank, 40 spherical poses; random-init Lego MLPs)",
+        "config": {"workload": "lego_800x800_64c_128f_train_step", "rays_per_gpu": R, "pts_per_ray": Pc + Pf,
+                   "global_batch_rays": R * world, "parallelism": f"dp{world}", "precision": args.precision},
+        "roofline": {"bound": "mfma", "kernel": "mlp_fwd_kernel (fine pass)", "achieved": round(achieved, 2),
+                     "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                     "flops_per_launch": fwd_flops, "avg_launch_ms": round(fwd_ms, 4)},
+        "step_mfma_tflops": round(flops_ray * value / world / 1e12, 2),
+        "step_mfma_frac": round(flops_ray * value / world / 1e12 / peak, 4),
+        "phase_ms": {k: round(v, 4) for k, v in probe.items()},
+        "train_psnr_synthetic": round(-10 * math.log10(max(mse_f, 1e-10)), 3),
+    }
+    del tr
+    if args.secondary not in ("", "none", args.precision):
+        tr2, dt2, _ = run(args.secondary, args.steps, args.warmup, probes=True)
+        p2 = tr2.probe_ms()
+        v2 = R * world * args.steps / dt2
+        f2 = p2.get("mlp_fwd_1", float("nan"))
+        ach2 = fwd_flops / (f2 * 1e-3) / 1e12
+        result["secondary"] = {
+            "precision": args.secondary, "value": round(v2, 1), "unit": "rays/s",
+            "ms_per_step": round(1e3 * dt2 / args.steps, 3),
+            "roofline": {"achieved": round(ach2, 2), "peak": PEAK_TFLOPS[args.secondary],
+                         "frac": round(ach2 / PEAK_TFLOPS[args.secondary], 4), "avg_launch_ms": round(f2, 4)},
+            "step_mfma_frac": round(flops_ray * v2 / world / 1e12 / PEAK_TFLOPS[args.secondary], 4),
+            "phase_ms": {k: round(v, 4) for k, v in p2.items()},
+            "note": "throughput mode: bf16 weights/activations, fp32 accumulate; parity-gated only loosely",
+        }
+        del tr2
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(pcfg, Pc, Pf - Pc)
+        result["vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
+    if rank == 0:
+        print(json.dumps(result))
+    parallel.barrier()
+    if parallel.is_dist():
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -359,10 +359,24 @@ def gen_zero_outputer(out):
                                 rendered_images=np32(preds["rendered_images"]), objective=np32(preds["objective"]))
 
 
+def gen_init_checksums(out):
+    """Seeded initialisation of the reference NeRFMLP (nerf_mlp.py:50-83, 244-261; _xavier_init :292-296)."""
+    d = dict(seed=np.int64(1234))
+    for tag, arch in (("lego", LEGO_ARCH), ("small", SMALL_ARCH)):
+        cfg = dict(type="NeRFMLP", **arch, harmonic_functions_xyz_append_intput=True,
+                   harmonic_functions_dir_append_intput=True, latent_dim=0, input_xyz=True, input_dir=True)
+        torch.manual_seed(1234)
+        m = MODELS.build(Config(dict(model=cfg)).model)
+        names = list(m.state_dict().keys())
+        d[f"{tag}_names"] = np.array(names)
+        d[f"{tag}_sums"] = np.array([m.state_dict()[k].double().sum().item() for k in names])
+    out["init_checksums"] = d
+
+
 def main():
     out = {}
     for f in (gen_harmonic, gen_raysampler, gen_mlp, gen_raymarcher, gen_sample_pdf, gen_render_eval,
-              gen_train_step, gen_zero_outputer):
+              gen_train_step, gen_zero_outputer, gen_init_checksums):
         f(out)
         print("generated", f.__name__)
     for name, d in out.items():

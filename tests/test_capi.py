@@ -1,0 +1,92 @@
+"""The C-ABI library builds, loads without a GPU and exports every entry point include/yanerf_hip.h declares;
+host-side argument validation and size queries behave (no kernel launches here)."""
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+import yanerf_boot  # noqa: F401
+from yanerf_amd import _C
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "yanerf_hip.h"
+
+
+def header_functions():
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"^\s*(?:const char\*|int64_t|int)\s+(yanerf_\w+)\s*\(", text, re.M)))
+
+
+def test_header_and_binding_agree():
+    assert set(header_functions()) == set(_C.EXPORTS)
+
+
+def test_library_exports_every_symbol():
+    lib = _C.lib()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_C.LIB_PATH)], capture_output=True, text=True, check=True)
+    exported = {line.split()[-1] for line in out.stdout.splitlines() if " T " in line}
+    missing = set(header_functions()) - exported
+    assert not missing, missing
+
+
+def test_struct_layout_matches_c(tmp_path):
+    """ctypes structs == the C header's layout (compiled with gcc against include/yanerf_hip.h)."""
+    src = tmp_path / "layout.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "yanerf_hip.h"\n'
+        "int main(){printf(\"%zu %zu %zu %zu %zu\\n\", sizeof(yanerf_mlp_desc), sizeof(yanerf_raymarch_opts),"
+        " offsetof(yanerf_raymarch_opts, bg_default), offsetof(yanerf_raymarch_opts, seed),"
+        " offsetof(yanerf_raymarch_opts, noise_std));return 0;}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert vals == [ctypes.sizeof(_C.MlpDesc), ctypes.sizeof(_C.RaymarchOpts), _C.RaymarchOpts.bg_default.offset,
+                    _C.RaymarchOpts.seed.offset, _C.RaymarchOpts.noise_std.offset]
+
+
+def lego_desc(**kw):
+    d = dict(n_layers=8, skip_mask=1 << 5, n_freq_xyz=10, n_freq_dir=4, append_xyz=1, append_dir=1, hidden_xyz=256,
+             hidden_dir=128, color_dim=3)
+    d.update(kw)
+    return _C.MlpDesc(*d.values())
+
+
+def test_mlp_size_queries():
+    L = _C.lib()
+    d = lego_desc()
+    assert L.yanerf_mlp_num_params(ctypes.byref(d)) == 24
+    f32 = L.yanerf_mlp_packed_bytes(ctypes.byref(d), _C.PREC_F32)
+    bf = L.yanerf_mlp_packed_bytes(ctypes.byref(d), _C.PREC_BF16)
+    assert f32 > bf > 0
+    # saved activations grow linearly with the point count (rounded up to the kernel's point tile)
+    s1 = L.yanerf_mlp_saved_bytes(ctypes.byref(d), _C.PREC_F32, 64)
+    s2 = L.yanerf_mlp_saved_bytes(ctypes.byref(d), _C.PREC_F32, 128)
+    assert s2 == 2 * s1 and L.yanerf_mlp_saved_bytes(ctypes.byref(d), _C.PREC_F32, 65) == s2
+    assert L.yanerf_mlp_bwd_workspace_bytes(ctypes.byref(d), _C.PREC_BF16, 1 << 20) > 0
+
+
+@pytest.mark.parametrize("bad,msg", [
+    (dict(n_freq_xyz=11), "xyz embedding"), (dict(n_freq_dir=5), "dir embedding"), (dict(hidden_xyz=300), "xyz"),
+    (dict(hidden_dir=256), "dir"), (dict(n_layers=0), "n_layers"), (dict(color_dim=5), "color_dim"),
+    (dict(skip_mask=1), "skip")])
+def test_mlp_desc_validation(bad, msg):
+    L = _C.lib()
+    d = lego_desc(**bad)
+    assert L.yanerf_mlp_num_params(ctypes.byref(d)) == -1
+    assert msg in L.yanerf_last_error().decode()
+
+
+def test_argument_validation_returns_error_without_launch():
+    L = _C.lib()
+    o = _C.RaymarchOpts()
+    o.bg_default_n = 1
+    assert L.yanerf_composite_forward(ctypes.byref(o), None, None, None, None, None, None, 4, 1000, 3, None, None,
+                                      None, None, None) == 1
+    assert "P=1000" in L.yanerf_last_error().decode()
+    assert L.yanerf_refine(None, None, 4, 2, 8, 1, None, 0, 0, 1, None, None) == 1
+    assert L.yanerf_raygen(None, None, None, None, 1, 1, 1, 1, 1.0, 1.0, 0.0, 1.0, 4, 0, None, 0, 0, None, None, None,
+                           None, None, None) == 1

@@ -1,0 +1,57 @@
+"""Data-parallel plumbing over torch.distributed with the gloo backend on CPU, world_size 2 (the GPU runs use
+the same code over RCCL): flat-buffer gradient all-reduce (DDP mean), parameter broadcast, metric all_gather,
+max-over-ranks timing, ray/image sharding."""
+import os
+import socket
+
+import torch
+import torch.multiprocessing as mp
+
+import yanerf_boot  # noqa: F401
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from yanerf_amd import parallel
+    r, w, _ = parallel.init_distributed(backend="gloo")
+    assert (r, w) == (rank, world)
+    torch.manual_seed(100 + rank)  # different init per rank
+    lin = [torch.nn.Parameter(torch.randn(5, 3)), torch.nn.Parameter(torch.randn(7))]
+    fp = parallel.FlatParams(lin)
+    parallel.broadcast_(fp.data)
+    fp.grad.copy_(torch.arange(fp.numel, dtype=torch.float32) * (rank + 1))
+    parallel.allreduce_mean_(fp.grad)
+    m = parallel.allgather_cat(torch.tensor([float(rank)]))
+    mx = parallel.max_over_ranks(float(rank) + 0.5)
+    shards = [list(parallel.shard_range(10, k, world)) for k in range(world)]
+    q.put((rank, fp.data.clone(), lin[0].grad.clone(), m, mx, shards))
+    parallel.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, d0, g0, m0, x0, s0), (_, d1, g1, m1, x1, s1) = res
+    assert torch.equal(d0, d1)  # broadcast from rank 0
+    expect = torch.arange(15, dtype=torch.float32).view(5, 3) * 1.5  # mean of x1 and x2
+    assert torch.allclose(g0, expect) and torch.allclose(g1, expect)
+    assert torch.equal(m0, torch.tensor([0.0, 1.0])) and x0 == x1 == 1.5
+    assert sorted(sum(s0, [])) == list(range(10))

@@ -539,81 +539,162 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
 }
 
 // ============================================================================================ backward dW
+// dW_l[n][k] = sum_points dZ_l[n][p] * X_l[k][p] (+ bias column: sum_points dZ_l[n][p]), both operands stored
+// feature-major ([row][point], written by the forward / dX kernels). One workgroup owns a [BN x 128] tile of
+// dW for a contiguous split of the points: per stage it stages 128-byte row segments (2 K-blocks) of the BN
+// dZ rows and the 128 X rows into LDS once (coalesced 16-B loads, next stage prefetched into registers while
+// the current one is multiplied), XOR-swizzled so the 16 rows a ds_read_b128 group touches hit distinct bank
+// slots; 8 waves tile the output (BN/64) x (8*64/BN). The bias gradient is a VALU row-sum of the staged dZ
+// rows in the k-tile-0 workgroups. Partial tiles go to per-split fp32 slabs; dw_reduce sums them in split
+// order (deterministic) straight into the reference-layout gradient tensors.
 struct DwJob {
-  const void* A;
+  const void* A;  // dZ rows [a_rows][Npad]
   int a_rows;
-  const void* X0;
+  const void* X0;  // layer input rows: segment 0 then segment 1
   int x0_rows;
   const void* X1;
   int x1_rows;
-  int kv;  // x0 + x1 + 1 (ones row -> bias)
-  int n_tiles, k_tiles, tile_base;
+  int ktot;  // x0 + x1 ; slab row length = ktot + 1 (bias column)
+  int bn;    // 256 | 128 | 64 rows per tile
+  int k_tiles, tile_base;
   int64_t slab_off;
-  float* W0;
-  float* b0;
-  int r0_begin, r0_count;
-  float* W1;
-  float* b1;
-  int r1_begin, r1_count;
+  float* W;  // grad of weight [a_rows][ktot] (reference layout)
+  float* b;  // grad of bias [a_rows]
 };
-constexpr int kMaxDwJobs = MAXL + 3;
+constexpr int kMaxDwJobs = MAXL + 4;
 struct DwJobs {
   DwJob j[kMaxDwJobs];
   int n;
   int total_tiles;
   int64_t slab_elems;
 };
+constexpr int DW_BK = 128, DW_THREADS = 512;
+
+template <typename T> __device__ __forceinline__ float hsum16(f4 v);
+template <> __device__ __forceinline__ float hsum16<float>(f4 v) { return (v.x + v.y) + (v.z + v.w); }
+template <> __device__ __forceinline__ float hsum16<bf16_t>(f4 v) {
+  us8 h = __builtin_bit_cast(us8, v);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s += bf2f(h[i]);
+  return s;
+}
+
+template <typename T, int BN>
+__device__ __forceinline__ void dw_tile(const DwJob& J, int kt, int s, int S, int64_t Npad, float* __restrict__ slab,
+                                        int64_t slab_elems, char* smem) {
+  constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
+  constexpr int WN = BN / 64, WK = 8 / WN, WKW = DW_BK / WK, KTW = WKW / 16;
+  constexpr int ROWS = BN + DW_BK, PER = ROWS * 8 / DW_THREADS;
+  static_assert(ROWS * 8 % DW_THREADS == 0, "staging split");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int wn = wave / WK, wk = wave % WK;
+  const int k0 = kt * DW_BK;
+  constexpr int SPTS = 2 * KB;  // points per stage (128 B per row)
+  const int64_t nst = Npad / SPTS;
+  const int64_t st_lo = nst * s / S, st_hi = nst * (s + 1) / S;
+  const T* src[PER];
+  int lrow[PER], lch[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int idx = tid + DW_THREADS * i;
+    const int row = idx >> 3, ch = idx & 7;
+    lrow[i] = row;
+    lch[i] = ch;
+    const T* p = nullptr;
+    if (row < BN) {
+      if (row < J.a_rows) p = (const T*)J.A + (int64_t)row * Npad;
+    } else {
+      const int k = k0 + row - BN;
+      if (k < J.x0_rows) p = (const T*)J.X0 + (int64_t)k * Npad;
+      else if (k < J.x0_rows + J.x1_rows) p = (const T*)J.X1 + (int64_t)(k - J.x0_rows) * Npad;
+    }
+    src[i] = p ? p + ch * EPC : nullptr;
+  }
+  const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
+  f4 regs[PER];
+  float rsum[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) rsum[i] = 0.f;
+  const bool do_bias = (kt == 0);
+  f4 acc[4][KTW];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int q = 0; q < KTW; ++q) acc[nt][q] = zero;
+  if (st_lo < st_hi) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) regs[i] = src[i] ? *(const f4*)(src[i] + st_lo * SPTS) : zero;
+  }
+  for (int64_t st = st_lo; st < st_hi; ++st) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      *(f4*)(smem + lrow[i] * 128 + ((lch[i] ^ ((lrow[i] >> 1) & 7)) << 4)) = regs[i];
+      if (do_bias && lrow[i] < BN) rsum[i] += hsum16<T>(regs[i]);
+    }
+    __syncthreads();
+    if (st + 1 < st_hi) {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) regs[i] = src[i] ? *(const f4*)(src[i] + (st + 1) * SPTS) : zero;
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int c = kb * 4 + g;
+      f4 a[4], b[KTW];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int row = wn * 64 + 16 * nt + li;
+        a[nt] = *(const f4*)(smem + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int q = 0; q < KTW; ++q) {
+        const int row = BN + wk * WKW + 16 * q + li;
+        b[q] = *(const f4*)(smem + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int q = 0; q < KTW; ++q) acc[nt][q] = mma_blk<T>(a[nt], b[q], acc[nt][q]);
+    }
+  }
+  float* out = slab + (int64_t)s * slab_elems + J.slab_off;
+  const int kv = J.ktot + 1;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int q = 0; q < KTW; ++q) {
+      const int k = k0 + wk * WKW + 16 * q + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = wn * 64 + 16 * nt + 4 * g + r;
+        if (n < J.a_rows && k < J.ktot) out[(int64_t)n * kv + k] = acc[nt][q][r];
+      }
+    }
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      float v = rsum[i];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      if (lch[i] == 0 && lrow[i] < BN && lrow[i] < J.a_rows) out[(int64_t)lrow[i] * kv + J.ktot] = v;
+    }
+  }
+}
 
 template <typename T>
-__global__ void __launch_bounds__(256) mlp_dw_kernel(DwJobs jobs, int64_t Npad, int S, float* __restrict__ slab) {
-  constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
+__global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t Npad, int S, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) char smem[(256 + DW_BK) * 128];
   const int tile = blockIdx.x, s = blockIdx.y;
   int ji = 0;
   while (ji + 1 < jobs.n && jobs.j[ji + 1].tile_base <= tile) ++ji;
   const DwJob& J = jobs.j[ji];
-  const int lt = tile - J.tile_base;
-  const int n0 = (lt / J.k_tiles) * 64, k0 = (lt % J.k_tiles) * 64;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  const int64_t nblk = Npad / KB;
-  const int64_t b_lo = nblk * s / S, b_hi = nblk * (s + 1) / S;
-  const int an = n0 + 16 * wave + li;
-  const T* arow = (an < J.a_rows) ? (const T*)J.A + (int64_t)an * Npad : nullptr;
-  const T* xrow[4];
-  bool ones[4];
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt) {
-    const int k = k0 + 16 * kt + li;
-    xrow[kt] = nullptr;
-    ones[kt] = false;
-    if (k < J.x0_rows) xrow[kt] = (const T*)J.X0 + (int64_t)k * Npad;
-    else if (k < J.x0_rows + J.x1_rows) xrow[kt] = (const T*)J.X1 + (int64_t)(k - J.x0_rows) * Npad;
-    else if (k == J.kv - 1) ones[kt] = true;
-  }
-  f4 onev;
-  if constexpr (sizeof(T) == 4) onev = f4{1.f, 1.f, 1.f, 1.f};
-  else onev = __builtin_bit_cast(f4, us8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80});
-  const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
-  f4 acc[4] = {zero, zero, zero, zero};
-  for (int64_t blk = b_lo; blk < b_hi; ++blk) {
-    const int64_t pb = blk * KB + g * EPC;
-    f4 a = arow ? *(const f4*)(arow + pb) : zero;
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      f4 b = xrow[kt] ? *(const f4*)(xrow[kt] + pb) : (ones[kt] ? onev : zero);
-      acc[kt] = mma_blk<T>(a, b, acc[kt]);
-    }
-  }
-  float* out = slab + (int64_t)s * jobs.slab_elems + J.slab_off;
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt) {
-    const int k = k0 + 16 * kt + li;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0 + 16 * wave + 4 * g + r;
-      if (n < J.a_rows && k < J.kv) out[(int64_t)n * J.kv + k] = acc[kt][r];
-    }
-  }
+  const int kt = tile - J.tile_base;
+  if (J.bn == 256) dw_tile<T, 256>(J, kt, s, S, Npad, slab, jobs.slab_elems, smem);
+  else if (J.bn == 128) dw_tile<T, 128>(J, kt, s, S, Npad, slab, jobs.slab_elems, smem);
+  else dw_tile<T, 64>(J, kt, s, S, Npad, slab, jobs.slab_elems, smem);
 }
 
 __global__ void dw_reduce_kernel(DwJobs jobs, int S, const float* __restrict__ slab) {
@@ -623,17 +704,12 @@ __global__ void dw_reduce_kernel(DwJobs jobs, int S, const float* __restrict__ s
   while (ji + 1 < jobs.n && jobs.j[ji + 1].slab_off <= e) ++ji;
   const DwJob& J = jobs.j[ji];
   const int64_t local = e - J.slab_off;
-  const int n = (int)(local / J.kv), k = (int)(local % J.kv);
+  const int kv = J.ktot + 1;
+  const int n = (int)(local / kv), k = (int)(local % kv);
   float sum = 0.0f;
   for (int s = 0; s < S; ++s) sum += slab[(int64_t)s * jobs.slab_elems + e];
-  const int ktot = J.kv - 1;
-  if (n >= J.r0_begin && n < J.r0_begin + J.r0_count) {
-    if (k < ktot) J.W0[(int64_t)(n - J.r0_begin) * ktot + k] = sum;
-    else J.b0[n - J.r0_begin] = sum;
-  } else if (J.W1 && n >= J.r1_begin && n < J.r1_begin + J.r1_count) {
-    if (k < ktot) J.W1[(int64_t)(n - J.r1_begin) * ktot + k] = sum;
-    else J.b1[n - J.r1_begin] = sum;
-  }
+  if (k < J.ktot) J.W[(int64_t)n * J.ktot + k] = sum;
+  else J.b[n] = sum;
 }
 
 // ============================================================================================ host helpers
@@ -678,73 +754,67 @@ static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, const f
   return 0;
 }
 
-static int dw_splits(int total_tiles, int64_t nblk) {
-  int64_t S = (2048 + total_tiles - 1) / total_tiles;
-  if (S > nblk) S = nblk;
+static int dw_splits(int total_tiles, int64_t n_stages) {
+  int64_t S = (1024 + total_tiles - 1) / total_tiles;
+  if (S > n_stages) S = n_stages;
   if (S > 64) S = 64;
   if (S < 1) S = 1;
   return (int)S;
 }
 
+static int dw_bn(int a_rows) { return a_rows > 128 ? 256 : (a_rows > 64 ? 128 : 64); }
+
+// enumerate the dW jobs (shared by the size query and the launch)
+template <typename F>
+static void for_each_dw_job(const MlpLayout& L, F&& f) {
+  const SavedRows SR = saved_rows(L.L);
+  const GradRows GR = grad_rows(L.L);
+  for (int l = 0; l < L.L; ++l) {
+    const int nout = (l + 1 < L.L) ? 256 : L.hid;
+    const bool sk = (L.skip >> l) & 1u;
+    if (l == 0) f(GR.dz0, nout, SR.pe, L.xyz_dim, -1, 0, 2 * l);
+    else if (sk) f(GR.dz0 + 256LL * l, nout, SR.h0 + 256LL * (l - 1), 256, SR.pe, L.xyz_dim, 2 * l);
+    else f(GR.dz0 + 256LL * l, nout, SR.h0 + 256LL * (l - 1), 256, -1, 0, 2 * l);
+  }
+  const int h = 2 * L.L;
+  f(GR.dyx, L.hid, SR.h0 + 256LL * (L.L - 1), L.hid, -1, 0, h + 0);        // intermediate_linear
+  f(GR.dyx + 256, 1, SR.h0 + 256LL * (L.L - 1), L.hid, -1, 0, h + 2);      // density_layer
+  f(GR.dzc, L.hdir, SR.y, L.hid, SR.dpe, L.dir_dim, h + 4);               // color_layer.0 (LinearWithRepeat)
+  f(GR.du, L.cdim, SR.c, L.hdir, -1, 0, h + 6);                           // color_layer.2
+}
+
 static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void* gradbuf, int64_t Npad,
                           float* const* grads, DwJobs& D) {
   const size_t es = elem_size(prec);
-  const SavedRows SR = saved_rows(L.L);
-  const GradRows GR = grad_rows(L.L);
-  auto srow = [&](int64_t r) { return (const void*)((const char*)saved + r * Npad * es); };
+  auto srow = [&](int64_t r) { return r < 0 ? nullptr : (const void*)((const char*)saved + r * Npad * es); };
   auto grow = [&](int64_t r) { return (const void*)((const char*)gradbuf + r * Npad * es); };
   D.n = 0;
   D.total_tiles = 0;
   D.slab_elems = 0;
-  auto add = [&](const void* A, int a_rows, const void* X0, int x0, const void* X1, int x1, float* W0, float* b0,
-                 int r0b, int r0c, float* W1, float* b1, int r1b, int r1c) {
+  for_each_dw_job(L, [&](int64_t arow, int a_rows, int64_t x0, int x0_rows, int64_t x1, int x1_rows, int gi) {
     DwJob& j = D.j[D.n++];
-    j.A = A; j.a_rows = a_rows; j.X0 = X0; j.x0_rows = x0; j.X1 = X1; j.x1_rows = x1;
-    j.kv = x0 + x1 + 1;
-    j.n_tiles = (a_rows + 63) / 64;
-    j.k_tiles = (j.kv + 63) / 64;
+    j.A = grow(arow); j.a_rows = a_rows;
+    j.X0 = srow(x0); j.x0_rows = x0_rows; j.X1 = srow(x1); j.x1_rows = x1_rows;
+    j.ktot = x0_rows + x1_rows;
+    j.bn = dw_bn(a_rows);
+    j.k_tiles = (j.ktot + DW_BK - 1) / DW_BK;
     j.tile_base = D.total_tiles;
-    D.total_tiles += j.n_tiles * j.k_tiles;
+    D.total_tiles += j.k_tiles;
     j.slab_off = D.slab_elems;
-    D.slab_elems += (int64_t)a_rows * j.kv;
-    j.W0 = W0; j.b0 = b0; j.r0_begin = r0b; j.r0_count = r0c;
-    j.W1 = W1; j.b1 = b1; j.r1_begin = r1b; j.r1_count = r1c;
-  };
-  for (int l = 0; l < L.L; ++l) {
-    const int nout = (l + 1 < L.L) ? 256 : L.hid;
-    const bool sk = (L.skip >> l) & 1u;
-    const void* A = grow(GR.dz0 + 256LL * l);
-    if (l == 0) add(A, nout, srow(SR.pe), L.xyz_dim, nullptr, 0, grads[0], grads[1], 0, nout, nullptr, nullptr, 0, 0);
-    else if (sk)
-      add(A, nout, srow(SR.h0 + 256LL * (l - 1)), 256, srow(SR.pe), L.xyz_dim, grads[2 * l], grads[2 * l + 1], 0, nout,
-          nullptr, nullptr, 0, 0);
-    else
-      add(A, nout, srow(SR.h0 + 256LL * (l - 1)), 256, nullptr, 0, grads[2 * l], grads[2 * l + 1], 0, nout, nullptr,
-          nullptr, 0, 0);
-  }
-  float* const* h = grads + 2 * L.L;
-  add(grow(GR.dyx), 257, srow(SR.h0 + 256LL * (L.L - 1)), L.hid, nullptr, 0, h[0], h[1], 0, L.hid, h[2], h[3], 256, 1);
-  add(grow(GR.dzc), L.hdir, srow(SR.y), L.hid, srow(SR.dpe), L.dir_dim, h[4], h[5], 0, L.hdir, nullptr, nullptr, 0, 0);
-  add(grow(GR.du), L.cdim, srow(SR.c), L.hdir, nullptr, 0, h[6], h[7], 0, L.cdim, nullptr, nullptr, 0, 0);
+    D.slab_elems += (int64_t)a_rows * (j.ktot + 1);
+    j.W = grads[gi];
+    j.b = grads[gi + 1];
+  });
 }
 
 static int64_t dw_slab_elems_for(const MlpLayout& L, int* total_tiles) {
-  // mirror of build_dw_jobs' sizes
   int64_t e = 0;
   int tiles = 0;
-  auto acc = [&](int a_rows, int kin) {
-    int kv = kin + 1;
-    e += (int64_t)a_rows * kv;
-    tiles += ((a_rows + 63) / 64) * ((kv + 63) / 64);
-  };
-  for (int l = 0; l < L.L; ++l) {
-    const int nout = (l + 1 < L.L) ? 256 : L.hid;
-    const bool sk = (L.skip >> l) & 1u;
-    acc(nout, l == 0 ? L.xyz_dim : (sk ? 256 + L.xyz_dim : 256));
-  }
-  acc(257, L.hid);
-  acc(L.hdir, L.hid + L.dir_dim);
-  acc(L.cdim, L.hdir);
+  for_each_dw_job(L, [&](int64_t, int a_rows, int64_t, int x0_rows, int64_t, int x1_rows, int) {
+    const int ktot = x0_rows + x1_rows;
+    e += (int64_t)a_rows * (ktot + 1);
+    tiles += (ktot + DW_BK - 1) / DW_BK;
+  });
   if (total_tiles) *total_tiles = tiles;
   return e;
 }
@@ -777,8 +847,9 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   YN_LAUNCH_CHECK("mlp_backward_dx");
   DwJobs D;
   build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D);
-  const int S = dw_splits(D.total_tiles, Npad / Cfg<T>::KB);
-  hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)D.total_tiles, (unsigned)S), dim3(256), 0, st, D, Npad, S, slab);
+  const int S = dw_splits(D.total_tiles, Npad / (2 * Cfg<T>::KB));
+  hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)D.total_tiles, (unsigned)S), dim3(DW_THREADS), 0, st, D, Npad, S,
+                     slab);
   YN_LAUNCH_CHECK("mlp_backward_dw");
   hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((D.slab_elems + 255) / 256)), dim3(256), 0, st, D, S, slab);
   YN_LAUNCH_CHECK("mlp_backward_reduce");
@@ -834,7 +905,7 @@ int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, 
   int tiles = 0;
   int64_t se = dw_slab_elems_for(L, &tiles);
   const int64_t kb = precision == YANERF_PREC_F32 ? Cfg<float>::KB : Cfg<bf16_t>::KB;
-  int S = dw_splits(tiles, Npad / kb);
+  int S = dw_splits(tiles, Npad / (2 * kb));
   return grad_bytes + (int64_t)S * se * 4;
 }
 

@@ -1,0 +1,202 @@
+"""Fused NeRF training step on the HIP path.
+
+One step = the reference's train_one_epoch inner step (runners/apis.py:55-89) for one image per rank:
+ray sampling (ray_sampler.py:149-246) -> coarse NeRFMLP -> EA composite -> sample_pdf refine -> fine NeRFMLP
+-> composite -> objective = mse(fine) + mse(coarse) (nerf_pipeline.py:284-305) -> backward -> gradient
+all-reduce over ranks (DDP semantics, run.py:162-166) -> Adam (run.py:158-160).
+
+Every stage is a kernel of libyanerf_hip.so launched on the current stream with workspaces allocated once, so a
+step issues a fixed launch sequence with no host synchronisation and no autograd graph. The models are ordinary
+NeRFMLP modules whose parameters are views into one flat buffer (checkpoints keep the reference's state_dict).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from . import _C, ops, parallel
+from .pipelines.models import MODELS
+
+F32 = torch.float32
+
+
+def lr_at(runner_cfg, it: int) -> float:
+    """Warm-up then exponential/cosine decay (runners/utils.py:65-109, applied per iteration in apis.py:66-68)."""
+    init = float(runner_cfg["init_lr"])
+    warm = int(runner_cfg.get("warmup_steps", 0))
+    if it < warm:
+        wl = float(runner_cfg.get("warmup_lr", init))
+        return min(init, wl + (init - wl) * it / max(warm, 1))
+    if runner_cfg.get("lr_decay_type", "exponential") == "exponential":
+        return max(float(runner_cfg["min_lr"]),
+                   init * float(runner_cfg["lr_decay_rate"]) ** (it / float(runner_cfg["lr_decay_iters"])))
+    mn = float(runner_cfg["min_lr"])
+    return (init - mn) * 0.5 * (1.0 + math.cos(math.pi * (it / float(runner_cfg["lr_decay_iters"])) /
+                                               float(runner_cfg["num_iters"]))) + mn
+
+
+class _Pass:
+    """Workspaces of one render pass (coarse or fine) for R rays x P samples."""
+
+    def __init__(self, spec: ops.MlpSpec, R: int, P: int, dev):
+        d = spec.desc()
+        L = _C.lib()
+        self.desc = d
+        self.P = P
+        N = R * P
+        self.sigma = torch.empty(N, dtype=F32, device=dev)
+        self.rgb = torch.empty(N, spec.color_dim, dtype=F32, device=dev)
+        self.saved = torch.empty(L.yanerf_mlp_saved_bytes(ctypes.byref(d), spec.precision, N), dtype=torch.uint8,
+                                 device=dev)
+        self.feats = torch.empty(R, spec.color_dim, dtype=F32, device=dev)
+        self.depth = torch.empty(R, dtype=F32, device=dev)
+        self.alpha = torch.empty(R, dtype=F32, device=dev)
+        self.w = torch.empty(R, P, dtype=F32, device=dev)
+        self.sq = torch.empty(R, dtype=F32, device=dev)
+        self.g_feats = torch.empty(R, spec.color_dim, dtype=F32, device=dev)
+        self.g_sigma = torch.empty(R, P, dtype=F32, device=dev)
+        self.g_rgb = torch.empty(R, P, spec.color_dim, dtype=F32, device=dev)
+        self.ws_bytes = L.yanerf_mlp_bwd_workspace_bytes(ctypes.byref(d), spec.precision, N)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class NeRFTrainer:
+    def __init__(self, pipeline_cfg, *, precision: str = "fp32", device="cuda", lr: float = 5e-4,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 42,
+                 n_rays: Optional[int] = None):
+        self.dev = torch.device(device)
+        rs, rd, mc = pipeline_cfg["ray_sampler"], pipeline_cfg["renderer"], pipeline_cfg["model"]
+        self.R = int(n_rays or rs["n_rays_per_image_sampled_from_mask"])
+        self.Pc = int(rs["n_pts_per_ray_training"])
+        self.Pn = int(rd["n_pts_per_ray_fine_training"])
+        self.append = bool(rd.get("append_coarse_samples_to_fine", True))
+        self.Pf = self.Pc + self.Pn if self.append else self.Pn
+        self.near, self.far = float(rs["min_depth"]), float(rs["max_depth"])
+        self.W, self.H = int(rs["image_width"]), int(rs["image_height"])
+        self.stratified = bool(rs.get("stratified_point_sampling_training", True))
+        self.random_refine = bool(rd.get("stratified_sampling_coarse_training", True))
+        self.noise_std = float(rd.get("density_noise_std_train", 0.0))
+        self.march = ops.RaymarchCfg(
+            capping_function=rd.get("capping_function", "exponential"),
+            weight_function=rd.get("weight_function", "product"),
+            background_opacity=float(rd.get("background_opacity", 1e10)), blend_output=bool(rd.get("blend_output",
+                                                                                                  False)),
+            background_density_bias=float(rd.get("background_density_bias", 0.0)),
+            hard_background=bool(rd.get("hard_background", False)),
+            bg_color=tuple(float(x) for x in rd.get("bg_color", (0.0,))))
+        torch.manual_seed(seed)
+        mcfg = dict(mc)
+        mcfg["precision"] = precision
+        self.models = [MODELS.build(dict(mcfg)).to(self.dev) for _ in range(2)]  # coarse, fine
+        self.specs = [m.spec() for m in self.models]
+        self.params: List[List[torch.nn.Parameter]] = [m.hip_params() for m in self.models]
+        self.flat = parallel.FlatParams(self.params[0] + self.params[1])
+        parallel.broadcast_(self.flat.data)
+        self.exp_avg = torch.zeros_like(self.flat.data)
+        self.exp_avg_sq = torch.zeros_like(self.flat.data)
+        self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        self.step_count = 0
+        L = _C.lib()
+        self.packed = [torch.empty(L.yanerf_mlp_packed_bytes(ctypes.byref(s.desc()), s.precision), dtype=torch.uint8,
+                                   device=self.dev) for s in self.specs]
+        R = self.R
+        self.o = torch.empty(R, 3, dtype=F32, device=self.dev)
+        self.d = torch.empty(R, 3, dtype=F32, device=self.dev)
+        self.zc = torch.empty(R, self.Pc, dtype=F32, device=self.dev)
+        self.zf = torch.empty(R, self.Pf, dtype=F32, device=self.dev)
+        self.xys = torch.empty(R, 2, dtype=F32, device=self.dev)
+        self.passes = [_Pass(self.specs[0], R, self.Pc, self.dev), _Pass(self.specs[1], R, self.Pf, self.dev)]
+        self.ws = torch.empty(max(p.ws_bytes for p in self.passes), dtype=torch.uint8, device=self.dev)
+        self.grad_ptrs = [_C.ptr_array([p.grad.data_ptr() for p in ps]) for ps in self.params]
+        self.param_ptrs = [_C.ptr_array([p.data_ptr() for p in ps]) for ps in self.params]
+        self.events: Optional[Dict[str, List]] = None  # optional per-phase timing probes
+
+    # --------------------------------------------------------------------------------------- timing probes
+    def enable_probes(self, names: Sequence[str]):
+        self.events = {n: [] for n in names}
+
+    def _probe(self, name, fn):
+        if self.events is None or name not in self.events:
+            return fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        r = fn()
+        e.record()
+        self.events[name].append((s, e))
+        return r
+
+    def probe_ms(self) -> Dict[str, float]:
+        out = {}
+        for n, evs in (self.events or {}).items():
+            if evs:
+                out[n] = sum(s.elapsed_time(e) for s, e in evs) / len(evs)
+        return out
+
+    # --------------------------------------------------------------------------------------- one step
+    def step(self, pose: torch.Tensor, focal: torch.Tensor, image: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """pose [1,3,4] (or [1,4,4]), focal [1], image [1,H,W,3] resident on the device."""
+        L = _C.lib()
+        st = ops._stream()
+        R = self.R
+        pose = pose.reshape(1, -1, 4)[:, :3, :4].contiguous()
+        focal = focal.reshape(1).contiguous()
+        image = image.reshape(1, self.H, self.W, -1)
+        # pack the current parameters into the kernel layout (both models)
+        for i, s in enumerate(self.specs):
+            _C.check(L.yanerf_mlp_pack(ctypes.byref(s.desc()), s.precision, self.param_ptrs[i], _p(self.packed[i]),
+                                       st), "yanerf_mlp_pack")
+        # rays: uniform pixel sampling without replacement + stratified depths (Philox)
+        seed, off = ops.RNG.next(R * self.Pc)
+        _C.check(L.yanerf_raygen(_p(pose), _p(focal), None, None, 1, R, self.W, self.H, float(self.W), float(self.H),
+                                 self.near, self.far, self.Pc, 2 if self.stratified else 0, None, seed, off, _p(self.o),
+                                 _p(self.d), _p(self.zc), _p(self.xys), None, st), "yanerf_raygen")
+        scale = 1.0 / (R * 3)
+        out = {}
+        for k, (z, ps) in enumerate(((self.zc, self.passes[0]), (self.zf, self.passes[1]))):
+            spec = self.specs[k]
+            if k == 1:
+                seed, off = ops.RNG.next(R * self.Pn)
+                _C.check(L.yanerf_refine(_p(self.zc), _p(self.passes[0].w), R, self.Pc, self.Pn,
+                                         0 if self.random_refine else 1, None, seed, off, int(self.append),
+                                         _p(self.zf), st), "yanerf_refine")
+            P = ps.P
+            self._probe(f"mlp_fwd_{k}", lambda: _C.check(L.yanerf_mlp_forward(
+                ctypes.byref(ps.desc), spec.precision, _p(self.packed[k]), _p(self.o), _p(self.d), _p(z), R, P,
+                _p(ps.sigma), _p(ps.rgb), _p(ps.saved), st), "yanerf_mlp_forward"))
+            if self.noise_std > 0:
+                seed, off = ops.RNG.next(R * P)
+                o = self.march.opts(2, self.noise_std, seed, off)
+            else:
+                o = self.march.opts(0, 0.0)
+            _C.check(L.yanerf_composite_forward(ctypes.byref(o), _p(ps.sigma), _p(ps.rgb), _p(z), _p(self.d), None,
+                                                None, R, P, 3, _p(ps.feats), _p(ps.depth), _p(ps.alpha), _p(ps.w), st),
+                     "yanerf_composite_forward")
+            _C.check(L.yanerf_rgb_loss(_p(ps.feats), _p(image), _p(self.xys), 1, R, self.H, self.W, 3, scale,
+                                       _p(ps.sq), _p(ps.g_feats), st), "yanerf_rgb_loss")
+            _C.check(L.yanerf_composite_backward(ctypes.byref(o), _p(ps.sigma), _p(ps.rgb), _p(z), _p(self.d), None,
+                                                 None, _p(ps.g_feats), None, None, R, P, 3, _p(ps.g_sigma),
+                                                 _p(ps.g_rgb), st), "yanerf_composite_backward")
+            out["sq_coarse" if k == 0 else "sq_fine"] = ps.sq
+        for k in (1, 0):
+            ps, spec = self.passes[k], self.specs[k]
+            self._probe(f"mlp_bwd_{k}", lambda: _C.check(L.yanerf_mlp_backward(
+                ctypes.byref(ps.desc), spec.precision, _p(self.packed[k]), _p(ps.saved), _p(ps.rgb), _p(ps.g_sigma),
+                _p(ps.g_rgb), R, ps.P, self.grad_ptrs[k], _p(self.ws), st), "yanerf_mlp_backward"))
+        parallel.allreduce_mean_(self.flat.grad)
+        self.step_count += 1
+        _C.check(L.yanerf_adam(_p(self.flat.data), _p(self.flat.grad), _p(self.exp_avg), _p(self.exp_avg_sq),
+                               self.flat.numel, float(self.lr), float(self.betas[0]), float(self.betas[1]),
+                               float(self.eps), float(self.weight_decay), self.step_count, st), "yanerf_adam")
+        return out
+
+    @staticmethod
+    def objective(out: Dict[str, torch.Tensor]) -> torch.Tensor:
+        """mse(fine) + mse(coarse) from the per-ray squared errors (device tensor; no host sync)."""
+        n = out["sq_fine"].numel() * 3
+        return (out["sq_fine"].sum() + out["sq_coarse"].sum()) / n

@@ -221,6 +221,27 @@ template <> __device__ __forceinline__ f4 mma_blk<bf16_t>(f4 a, f4 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a), __builtin_bit_cast(bf8, b), c, 0, 0, 0);
 }
 
+// acc[i][j] += A_i x B_j over one 64-byte K-block for a grid of independent accumulators. fp32: the four
+// 16x16x4 k-steps are the OUTER loop so consecutive MFMAs never depend on each other (dependent-accumulator
+// latency 40 cycles > 32-cycle issue); bf16: one 16x16x32 per pair.
+template <typename T, int NI, int NJ>
+__device__ __forceinline__ void mma_grid(const f4 (&a)[NI], const f4 (&b)[NJ], f4 (&acc)[NI][NJ]) {
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mma_blk<T>(a[i], b[j], acc[i][j]);
+  }
+}
+
 // acc[nt][mt] (rows nrow0 + 16nt.., points 16mt..) = W[rows][kblocks] x act[points][kblocks]^T
 template <typename T, int NT, int MT>
 __device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int nrow0, const T* act, int kc0, int nkb,
@@ -245,10 +266,7 @@ __device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int n
     f4 b[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) b[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + kb * 4 + g);
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = mma_blk<T>(a[nt], b[mt], acc[nt][mt]);
+    mma_grid<T, NT, MT>(a, b, acc);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) a[nt] = an[nt];
   }
@@ -444,7 +462,6 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
   constexpr int NT = 256 / 16 / WAVES;
   constexpr int KB = Cfg<T>::KB;
   __shared__ __attribute__((aligned(16))) T act[M * ROW];
-  __shared__ float s_gs[M];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int64_t p0 = (int64_t)blockIdx.x * M;
@@ -466,7 +483,6 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
   if (q == 0) {
     for (int j = 0; j < cd; ++j) grad[(GR.du + j) * Npad + p] = to_t<T>(du[j]);
     grad[(GR.dyx + 256) * Npad + p] = to_t<T>(gs);
-    s_gs[mt_] = gs;
   }
   {
     const float* wo = Wf + lay.wo_off;
@@ -524,7 +540,10 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
       for (int mt = 0; mt < MT; ++mt) {
         const int m = 16 * mt + li;
         f4 v = acc[nt][mt];
-        if (l == lay.L) v = v + wdv * s_gs[m];
+        if (l == lay.L) {
+          const float gsm = (p0 + m < N) ? g_sigma[p0 + m] : 0.0f;
+          v = v + wdv * gsm;
+        }
         v.x = hm[nt][mt].x > 0.f ? v.x : 0.f;
         v.y = hm[nt][mt].y > 0.f ? v.y : 0.f;
         v.z = hm[nt][mt].z > 0.f ? v.z : 0.f;
@@ -653,10 +672,7 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int kt, int s, int S, in
         const int row = BN + wk * WKW + 16 * q + li;
         b[q] = *(const f4*)(smem + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
       }
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int q = 0; q < KTW; ++q) acc[nt][q] = mma_blk<T>(a[nt], b[q], acc[nt][q]);
+      mma_grid<T, 4, KTW>(a, b, acc);
     }
   }
   float* out = slab + (int64_t)s * slab_elems + J.slab_off;

@@ -103,6 +103,51 @@ def cpu_baseline(precision_cfg, n_pts_c: int, n_pts_f_new: int, budget_s: float 
                       f"in batches of {R}, numpy fp32 oracle, {dt:.1f} s"}
 
 
+def extras(pcfg, cfg, dev, poses, focal, image, precision):
+    """Secondary timings (not the headline): (1) full 800x800 evaluation render through the registry
+    NeRFPipeline (no_grad, the reference's 131072-point chunking), (2) one training step through the drop-in
+    path: registry NeRFPipeline + torch autograd + torch.optim.Adam, i.e. what scripts/run.py would run."""
+    import copy
+
+    from yanerf_amd.pipelines import PIPELINES
+    from yanerf_amd.pipelines.utils import EvaluationMode
+    out = {}
+    c = copy.deepcopy(pcfg)
+    c.model.precision = precision
+    pipe = PIPELINES.build(c).to(dev)
+    pipe.eval()
+    H = W = 800
+    with torch.no_grad():
+        pipe(poses=poses[:1], focal_lengths=focal, image_height=64, image_width=64,
+             evaluation_mode=EvaluationMode.EVALUATION)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pred = pipe(poses=poses[1:2], focal_lengths=focal, image_rgb=image, evaluation_mode=EvaluationMode.EVALUATION)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    out["eval_render"] = {"rays_per_s": round(H * W / dt, 1), "s_per_image": round(dt, 3),
+                          "psnr_vs_synthetic": round(-10 * math.log10(float(pred["loss_rgb_mse"].mean())), 3),
+                          "chunk_size_grid": int(c.chunk_size_grid), "precision": precision}
+    pipe.train()
+    opt = torch.optim.Adam(pipe.parameters(), lr=float(cfg.runner.init_lr))
+    steps = 5
+    for i in range(steps + 2):
+        if i == 2:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        preds = pipe(poses=poses[i:i + 1], focal_lengths=focal, image_rgb=image,
+                     evaluation_mode=EvaluationMode.TRAINING)
+        opt.zero_grad(set_to_none=True)
+        preds["objective"].mean().backward()
+        opt.step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    R = int(c.ray_sampler.n_rays_per_image_sampled_from_mask)
+    out["dropin_train"] = {"rays_per_s": round(R / dt, 1), "ms_per_step": round(1e3 * dt, 3), "precision": precision,
+                           "path": "registry NeRFPipeline + autograd + torch.optim.Adam"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -113,6 +158,7 @@ def main():
     ap.add_argument("--config", default=str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--secondary", default="bf16", help="also time this precision (reported under `secondary`)")
+    ap.add_argument("--no-extras", action="store_true", help="skip the eval-render and drop-in-path timings")
     args = ap.parse_args()
 
     rank, world, local = parallel.init_distributed()
@@ -208,6 +254,8 @@ def main():
             "note": "throughput mode: bf16 weights/activations, fp32 accumulate; parity-gated only loosely",
         }
         del tr2
+    if not args.no_extras:
+        result["extras"] = extras(pcfg, cfg, dev, poses, focal, image, args.precision)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(pcfg, Pc, Pf - Pc)
         result["vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)

@@ -340,3 +340,48 @@ def test_zero_outputer_known_answer(pkg, golden):
     assert torch.all(preds["rendered_images"] == bg)
     np.testing.assert_array_equal(n(preds["rendered_images"]), g["rendered_images"])
     assert torch.allclose(preds["objective"], torch.zeros(1, device=DEV))
+
+
+def test_fern_config_render_vs_oracle(pkg):
+    """Fern product config (64 + 64 samples, 504x378 configured grid) through the registry pipeline: coarse stage
+    strict against the oracle on a 6x8 override render (principal point from the configured size)."""
+    import yanerf_boot  # noqa: F401
+    from yanerf_amd.utils.config import Config
+    cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/fern.yml")).pipeline
+    pipe = pkg["PIPELINES"].build(cfg).to(DEV)
+    params = [make_nerf_mlp_params(LEGO_ARCH, s) for s in (41, 42)]
+    for f, p in zip(pipe.implicit_functions, params):
+        f._fn.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
+    pipe.eval()
+    pose = np.eye(4, dtype=np.float32)[:3].copy()
+    pose[2, 3] = 4.0
+    H, W = 6, 8
+    with torch.no_grad():
+        rb = pipe.ray_sampler(t(pose[None]), t([407.6]), evaluation_mode=pkg["EM"].EVALUATION, image_height=H,
+                              image_width=W)
+        ro = pipe.renderer(*rb, bg_color=None, implicit_functions=pipe.implicit_functions,
+                           evaluation_mode=pkg["EM"].EVALUATION)
+    o, d, z, _ = O.sample_rays_eval(pose[None], np.array([407.6], np.float32), 504, 378, 2.0, 6.0, 64, H=H, W=W)
+    R = H * W
+    ref = O.render_two_pass(params[0], params[1], O.MLPArch.from_dict(LEGO_ARCH),
+                            O.RenderCfg(n_pts_fine=64, raymarch=O.RaymarchOpts(background_density_bias=1e-6)),
+                            o.reshape(R, 3), d.reshape(R, 3), z.reshape(R, 64))
+    close(n(ro.prev_stage.features).reshape(R, 3), ref["coarse"][0], 1e-5)
+    close(n(ro.prev_stage.depths).reshape(R), ref["coarse"][1].reshape(R), 1e-4)
+    close_render(n(ro.features).reshape(R, 3), ref["fine"][0])
+
+
+def test_chunking_invariance(pkg, golden):
+    """The reference's ray chunking (nerf_pipeline.py:217-231, 333-377) must not change results."""
+    g = golden("render_eval_lego")
+    pipe = _lego_pipeline(pkg, g["seeds"])
+    pipe.eval()
+    kw = dict(poses=t(g["pose"]), focal_lengths=t(g["focal"]), image_height=16, image_width=16,
+              evaluation_mode=pkg["EM"].EVALUATION)
+    with torch.no_grad():
+        a = pipe(**kw)["rendered_images"]
+        pipe.chunk_size_grid = 5 * 256  # 5 rays per chunk
+        b = pipe(**kw)["rendered_images"]
+        pipe.chunk_size_grid = 0  # unchunked
+        c = pipe(**kw)["rendered_images"]
+    assert torch.equal(a, b) and torch.equal(a, c)

@@ -84,6 +84,21 @@ __host__ __device__ inline GradRows grad_rows(int L) {
   return g;
 }
 
+// ReLU masks, kept for the dX kernel instead of re-reading the saved activations:
+//  * trunk layers: the forward and dX kernels share one wave->tile decomposition (Cfg<T>), so every lane packs
+//    ITS OWN 4 bits of each of its NT*MT = 16 accumulator tiles into one u64 per layer
+//    (index ((layer * n_wg + wg) * WAVES + wave) * 64 + lane): one coalesced 8-byte load per lane in dX;
+//  * colour hidden layer: the __ballot of each 16x16 tile (4 u64 words; bit `lane` = feature 4*(lane>>4)+r of
+//    point lane&15), read per point by the VALU colour-head backward.
+// Both are 256 bits per point per layer.
+__host__ __device__ inline int64_t mask_words_per_slot(int64_t Npad) { return Npad / 16 * 16 * 4; }
+__device__ __forceinline__ int64_t mask_index(int64_t Npad, int slot, int64_t pt16, int ft) {
+  return (((int64_t)slot * (Npad / 16) + pt16) * 16 + ft) * 4;
+}
+static int64_t saved_t_bytes(int L, int64_t Npad, size_t es) {
+  return (saved_rows(L).rows * Npad * (int64_t)es + 255) / 256 * 256;
+}
+
 static int64_t tile_m(int prec) { return prec == YANERF_PREC_F32 ? Cfg<float>::M : Cfg<bf16_t>::M; }
 static int64_t npad_of(int prec, int64_t n) { int64_t M = tile_m(prec); return (n + M - 1) / M * M; }
 static size_t elem_size(int prec) { return prec == YANERF_PREC_F32 ? 4 : 2; }
@@ -297,16 +312,25 @@ __device__ __forceinline__ float pe_value(const float x[3], int k, int F, int ap
   return 0.0f;
 }
 
+__device__ __forceinline__ void store_mask_tile(uint64_t* masks, int64_t Npad, int slot, int64_t pt16, int ft, f4 v,
+                                                int lane) {
+  const uint64_t b0 = __ballot(v.x > 0.f), b1 = __ballot(v.y > 0.f), b2 = __ballot(v.z > 0.f),
+                 b3 = __ballot(v.w > 0.f);
+  if (lane < 4) masks[mask_index(Npad, slot, pt16, ft) + lane] = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
+}
+
 // ============================================================================================ forward
 template <typename T>
 __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
     MlpLayout lay, const T* __restrict__ Wt, const float* __restrict__ Wf, const float* __restrict__ origins,
     const float* __restrict__ dirs, const float* __restrict__ lengths, int64_t R, int64_t P,
-    float* __restrict__ sigma, float* __restrict__ rgb, T* __restrict__ saved, int64_t Npad) {
+    float* __restrict__ sigma, float* __restrict__ rgb, T* __restrict__ saved, uint64_t* __restrict__ masks,
+    int64_t Npad) {
   constexpr int M = Cfg<T>::M, WAVES = Cfg<T>::WAVES, MT = M / 16;
   constexpr int NT = 256 / 16 / WAVES, NTC = HC / 16 / WAVES;
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
   static_assert(M * 4 == WAVES * 64, "4 threads per point");
+  static_assert(NT * MT == 16, "per-lane mask word holds 16 tiles x 4 bits");
   __shared__ __attribute__((aligned(16))) T act[M * ROW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -343,6 +367,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
     gemm_lds<T, NT, MT>(Wt + lay.w_off[l], lay.kpad[l], nrow0, act, kc0, nkb, acc, lane);
     __syncthreads();
     const float* bias = Wf + lay.b_off[l];
+    uint64_t bits = 0;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int n = nrow0 + 16 * nt + 4 * g;
@@ -356,9 +381,13 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
         if (saved) {
           T* s = saved + (SR.h0 + 256LL * l + n) * Npad + p0 + m;
           s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
+          const int sh = (nt * MT + mt) * 4;
+          bits |= ((uint64_t)(v.x > 0.f) << sh) | ((uint64_t)(v.y > 0.f) << (sh + 1)) |
+                  ((uint64_t)(v.z > 0.f) << (sh + 2)) | ((uint64_t)(v.w > 0.f) << (sh + 3));
         }
       }
     }
+    if (saved) masks[(((int64_t)l * gridDim.x + blockIdx.x) * WAVES + wave) * 64 + lane] = bits;
     __syncthreads();
   }
   // ---- density head (VALU): sigma = w_d . h + b_d  (nerf_mlp.py:173; density_layer 256->1)
@@ -423,6 +452,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
         if (saved) {
           T* s = saved + (SR.c + n) * Npad + p0 + m;
           s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
+          store_mask_tile(masks + (int64_t)lay.L * mask_words_per_slot(Npad), Npad, 0, p0 / 16 + mt,
+                          (crow0 + 16 * nt) / 16, v, lane);
         }
       }
     }
@@ -456,16 +487,16 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
 template <typename T>
 __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
     MlpLayout lay, const T* __restrict__ Wt, const float* __restrict__ Wf, const T* __restrict__ saved,
-    const float* __restrict__ rgb, const float* __restrict__ g_sigma, const float* __restrict__ g_rgb, int64_t N,
-    int64_t Npad, T* __restrict__ grad) {
+    const uint64_t* __restrict__ masks, const float* __restrict__ rgb, const float* __restrict__ g_sigma,
+    const float* __restrict__ g_rgb, int64_t N, int64_t Npad, T* __restrict__ grad) {
   constexpr int M = Cfg<T>::M, WAVES = Cfg<T>::WAVES, MT = M / 16;
   constexpr int NT = 256 / 16 / WAVES;
   constexpr int KB = Cfg<T>::KB;
   __shared__ __attribute__((aligned(16))) T act[M * ROW];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int64_t p0 = (int64_t)blockIdx.x * M;
-  const SavedRows SR = saved_rows(lay.L);
   const GradRows GR = grad_rows(lay.L);
   const int mt_ = tid >> 2, q = tid & 3;
   const int64_t p = p0 + mt_;
@@ -486,11 +517,20 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
   }
   {
     const float* wo = Wf + lay.wo_off;
+    // colour-hidden ReLU masks for this point: feature tiles 2q, 2q+1 (slot L)
+    uint64_t cw[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cw[t][r] = masks[lay.L * mask_words_per_slot(Npad) + mask_index(Npad, 0, p / 16, 2 * q + t) + r];
     for (int c = 32 * q; c < 32 * q + 32; ++c) {
       float dc = 0.0f;
       for (int j = 0; j < cd; ++j) dc += du[j] * wo[j * HC + c];
-      float cval = to_f<T>(saved[(SR.c + c) * Npad + p]);
-      float dz = cval > 0.0f ? dc : 0.0f;
+      const int cl = c & 15;
+      const uint64_t word = cw[(c >> 4) & 1][cl & 3];
+      const bool on = (word >> (16 * (cl >> 2) + (mt_ & 15))) & 1ull;
+      float dz = on ? dc : 0.0f;
       act[lds_idx<T>(mt_, c)] = to_t<T>(dz);
       grad[(GR.dzc + c) * Npad + p] = to_t<T>(dz);
     }
@@ -519,16 +559,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
     // l == L: the heads -> last trunk layer; else trunk layer l -> layer l-1
     const T* A = (l == lay.L) ? Wt + lay.wintT_off : Wt + lay.wt_off[l];
     const int hl = l - 1;  // layer whose output gradient we form
-    // prefetch relu masks of H_{hl}
-    f4 hm[NT][MT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int n = nrow0 + 16 * nt + 4 * g, m = 16 * mt + li;
-        const T* s = saved + (SR.h0 + 256LL * hl + n) * Npad + p0 + m;
-        hm[nt][mt] = f4{to_f<T>(s[0]), to_f<T>(s[Npad]), to_f<T>(s[2 * Npad]), to_f<T>(s[3 * Npad])};
-      }
+    const uint64_t bits = masks[(((int64_t)hl * gridDim.x + blockIdx.x) * WAVES + wave) * 64 + lane];
     gemm_lds<T, NT, MT>(A, 256, nrow0, act, 0, 256 / KB, acc, lane);
     __syncthreads();
     const float* wd = Wf + lay.wd_off;
@@ -544,10 +575,12 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
           const float gsm = (p0 + m < N) ? g_sigma[p0 + m] : 0.0f;
           v = v + wdv * gsm;
         }
-        v.x = hm[nt][mt].x > 0.f ? v.x : 0.f;
-        v.y = hm[nt][mt].y > 0.f ? v.y : 0.f;
-        v.z = hm[nt][mt].z > 0.f ? v.z : 0.f;
-        v.w = hm[nt][mt].w > 0.f ? v.w : 0.f;
+        // ReLU mask of H_{hl}: this lane's own bits of this tile (packed by the forward)
+        const int sh = (nt * MT + mt) * 4;
+        v.x = ((bits >> sh) & 1ull) ? v.x : 0.f;
+        v.y = ((bits >> (sh + 1)) & 1ull) ? v.y : 0.f;
+        v.z = ((bits >> (sh + 2)) & 1ull) ? v.z : 0.f;
+        v.w = ((bits >> (sh + 3)) & 1ull) ? v.w : 0.f;
         lds_put4<T>(act, m, n, v);
         T* s = grad + (GR.dz0 + 256LL * hl + n) * Npad + p0 + m;
         s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
@@ -843,7 +876,9 @@ static int launch_fwd(const MlpLayout& L, const void* packed, const float* o, co
   const T* Wt = (const T*)packed;
   const float* Wf = (const float*)((const char*)packed + L.f_base);
   dim3 grid((unsigned)(Npad / Cfg<T>::M)), block(Cfg<T>::WAVES * 64);
-  hipLaunchKernelGGL(mlp_fwd_kernel<T>, grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, (T*)saved, Npad);
+  uint64_t* masks = saved ? (uint64_t*)((char*)saved + saved_t_bytes(L.L, Npad, sizeof(T))) : nullptr;
+  hipLaunchKernelGGL(mlp_fwd_kernel<T>, grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, (T*)saved, masks,
+                     Npad);
   YN_LAUNCH_CHECK("mlp_forward");
   return 0;
 }
@@ -858,8 +893,9 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   T* gradbuf = (T*)ws;
   int64_t grad_bytes = (GR.rows * Npad * (int64_t)sizeof(T) + 255) / 256 * 256;
   float* slab = (float*)((char*)ws + grad_bytes);
+  const uint64_t* masks = (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(T)));
   hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::WAVES * 64), 0, st, L, Wt,
-                     Wf, (const T*)saved, rgb, gs, gr, N, Npad, gradbuf);
+                     Wf, (const T*)saved, masks, rgb, gs, gr, N, Npad, gradbuf);
   YN_LAUNCH_CHECK("mlp_backward_dx");
   DwJobs D;
   build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D);
@@ -909,7 +945,8 @@ int yanerf_mlp_pack(const yanerf_mlp_desc* d, int precision, const float* const*
 
 int64_t yanerf_mlp_saved_bytes(const yanerf_mlp_desc* d, int precision, int64_t n_points) {
   if (check_desc(d)) return -1;
-  return saved_rows(d->n_layers).rows * npad_of(precision, n_points) * (int64_t)elem_size(precision);
+  const int64_t Npad = npad_of(precision, n_points);
+  return saved_t_bytes(d->n_layers, Npad, elem_size(precision)) + (d->n_layers + 1) * mask_words_per_slot(Npad) * 8;
 }
 
 int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, int64_t n_points) {

@@ -23,13 +23,19 @@
 // (3) a deterministic reduce sums the slabs straight into the reference-layout parameter gradients.
 #include "common.hpp"
 
+// Development-only timing ablations (never set in the product build): 1 = no MFMA, 2 = no harmonic embedding,
+// 4 = no bias/ReLU/saved stores in the trunk epilogue, 8 = no VALU heads.
+#ifndef YANERF_ABLATE
+#define YANERF_ABLATE 0
+#endif
+
 namespace yanerf {
 
 typedef unsigned short bf16_t;
 
 template <typename T> struct Cfg;
-template <> struct Cfg<float> { static constexpr int M = 64, WAVES = 4, EPC = 4, KB = 16; };
-template <> struct Cfg<bf16_t> { static constexpr int M = 128, WAVES = 8, EPC = 8, KB = 32; };
+template <> struct Cfg<float> { static constexpr int M = 64, WAVES = 4, EPC = 4, KB = 16, APREF = 1; };
+template <> struct Cfg<bf16_t> { static constexpr int M = 128, WAVES = 8, EPC = 8, KB = 32, APREF = 3; };
 
 constexpr int ROW = 320;    // LDS row length (elements)
 constexpr int PE_COL = 256; // xyz-PE / dir-PE column base
@@ -200,8 +206,13 @@ __global__ void pack_kernel(PackJobs jobs, T* __restrict__ dst_t, float* __restr
   if (J.is_f32) {
     dst_f[J.dst_off + local] = v;
   } else {
-    if constexpr (sizeof(T) == 4) dst_t[J.dst_off + local] = v;
-    else dst_t[J.dst_off + local] = f2bf(v);
+    // GEMM operands are stored in MFMA A-fragment order: for each 16-row tile and 64-byte K-block, 64 lanes x 16 B,
+    // lane = 16 * (k-chunk) + (row within the tile), so one wave-wide 16-byte load reads 1 KiB contiguously
+    constexpr int KB = Cfg<T>::KB, EPC = Cfg<T>::EPC;
+    const int64_t fi = (((int64_t)(r >> 4) * (J.cols / KB) + c / KB) * 64 + ((c % KB) / EPC) * 16 + (r & 15)) * EPC +
+                       c % EPC;
+    if constexpr (sizeof(T) == 4) dst_t[J.dst_off + fi] = v;
+    else dst_t[J.dst_off + fi] = f2bf(v);
   }
 }
 
@@ -241,6 +252,13 @@ template <> __device__ __forceinline__ f4 mma_blk<bf16_t>(f4 a, f4 b, f4 c) {
 // latency 40 cycles > 32-cycle issue); bf16: one 16x16x32 per pair.
 template <typename T, int NI, int NJ>
 __device__ __forceinline__ void mma_grid(const f4 (&a)[NI], const f4 (&b)[NJ], f4 (&acc)[NI][NJ]) {
+  if constexpr (YANERF_ABLATE & 1) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] += a[i] * b[j].x;
+    return;
+  }
   if constexpr (sizeof(T) == 4) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -258,6 +276,11 @@ __device__ __forceinline__ void mma_grid(const f4 (&a)[NI], const f4 (&b)[NJ], f
 }
 
 // acc[nt][mt] (rows nrow0 + 16nt.., points 16mt..) = W[rows][kblocks] x act[points][kblocks]^T
+//
+// bf16: a K-block is only 16 MFMAs per wave (256 cycles), shorter than an L2 round trip, so the weight fragments
+// stream through a register ring APREF K-blocks deep and the LDS fragments of block kb+1 are read while block kb
+// multiplies (the loop is unrolled by the ring depth so every ring slot is a static register set). Loads past the
+// last K-block re-read the last block (uniform, in-bounds, a few redundant L2 hits per layer).
 template <typename T, int NT, int MT>
 __device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int nrow0, const T* act, int kc0, int nkb,
                                          f4 (&acc)[NT][MT], int lane) {
@@ -267,9 +290,51 @@ __device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int n
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f4{0.f, 0.f, 0.f, 0.f};
+  // W is in A-fragment order (pack_kernel): row tile rt, K-block kb at ((rt * ldw / KB + kb) * 64 + lane) * EPC
   const T* wp[NT];
+  constexpr int FRAG = 64 * EPC;
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) wp[nt] = W + (size_t)(nrow0 + 16 * nt + li) * ldw + g * EPC;
+  for (int nt = 0; nt < NT; ++nt) wp[nt] = W + ((size_t)((nrow0 >> 4) + nt) * (ldw / KB) * 64 + lane) * EPC;
+  if constexpr (sizeof(T) == 2) {
+    constexpr int D = Cfg<T>::APREF;
+    f4 a[D][NT];
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      const int k = r < nkb ? r : nkb - 1;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) a[r][nt] = *(const f4*)(wp[nt] + k * FRAG);
+    }
+    f4 b[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) b[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + g);
+    // one K-block: read block kb+1's LDS fragments, multiply block kb, refill the ring slot with block kb+D
+    auto step = [&](int kb, f4(&ar)[NT], bool refill) {
+      const int kn = kb + 1 < nkb ? kb + 1 : kb;
+      f4 bn[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) bn[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + kn * 4 + g);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_grid<T, NT, MT>(ar, b, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      if (refill) {
+        const int ka = kb + D < nkb ? kb + D : nkb - 1;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) ar[nt] = *(const f4*)(wp[nt] + ka * FRAG);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) b[mt] = bn[mt];
+    };
+    int kb = 0;
+    for (; kb + D <= nkb; kb += D) {
+#pragma unroll
+      for (int r = 0; r < D; ++r) step(kb + r, a[r], true);
+    }
+    // tail of nkb % D blocks, straight-line (ring slot r holds block kb + r)
+#pragma unroll
+    for (int r = 0; r < D - 1; ++r)
+      if (kb + r < nkb) step(kb + r, a[r], false);
+    return;
+  }
   f4 a[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) a[nt] = *(const f4*)(wp[nt]);
@@ -277,7 +342,7 @@ __device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int n
     f4 an[NT];
     const int kn = (kb + 1 < nkb) ? kb + 1 : kb;
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) an[nt] = *(const f4*)(wp[nt] + kn * KB);
+    for (int nt = 0; nt < NT; ++nt) an[nt] = *(const f4*)(wp[nt] + kn * FRAG);
     f4 b[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) b[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + kb * 4 + g);
@@ -297,19 +362,60 @@ template <> __device__ __forceinline__ void lds_put4<bf16_t>(bf16_t* act, int m,
   *(us4*)(act + m * ROW + swz<bf16_t>(m, n / 8) * 8 + (n & 7)) = h;
 }
 
-// harmonic embedding element k of 3-vector x (models/utils.py:98-102): [sin(x_i 2^f) i-major f-minor, cos, x]
-__device__ __forceinline__ float pe_value(const float x[3], int k, int F, int append) {
-  if (k < 3 * F) {
-    int i = k / F, f = k % F;
-    return sinf(x[i] * (float)(1 << f));
+// Harmonic embedding (models/utils.py:98-102) of 3-vector x: columns [sin(x_i 2^f) i-major f-minor | cos(...) | x],
+// zero-padded to `width`, written into LDS row m at column col0 (and, when `sv` is set, into feature-major saved
+// rows sv[k * Npad]). The 4 threads of a point share the work: thread q takes the (i, f) pairs j = q, q+4, ...
+// and one sincosf per pair yields both the sin column j and the cos column 3F + j.
+template <typename T>
+__device__ __forceinline__ void harmonic_to_lds(T* act, int m, int col0, int width, const float x[3], int F,
+                                                int append, int q, T* sv, int64_t Npad) {
+  for (int j = q; j < 3 * F; j += 4) {
+    const int i = j / F, f = j - i * F;
+    float xi = x[0];
+    xi = i == 1 ? x[1] : xi;
+    xi = i == 2 ? x[2] : xi;
+    float sn, cs;
+    if constexpr (sizeof(T) == 4) {
+      sincosf(xi * (float)(1 << f), &sn, &cs);  // the parity mode keeps libm-accurate sin/cos
+    } else {
+      // bf16 mode: reduce to revolutions and use the hardware sin/cos (|error| ~1e-4 rad at the largest
+      // frequency, far below the 2^-9 relative rounding of the bf16 value it feeds)
+      float r = xi * (float)(1 << f) * 0.15915494309189535f;
+      r -= rintf(r);
+      sn = __builtin_amdgcn_sinf(r);
+      cs = __builtin_amdgcn_cosf(r);
+    }
+    act[lds_idx<T>(m, col0 + j)] = to_t<T>(sn);
+    act[lds_idx<T>(m, col0 + 3 * F + j)] = to_t<T>(cs);
+    if (sv) {
+      sv[(int64_t)j * Npad] = to_t<T>(sn);
+      sv[(int64_t)(3 * F + j) * Npad] = to_t<T>(cs);
+    }
   }
-  if (k < 6 * F) {
-    int kk = k - 3 * F;
-    int i = kk / F, f = kk % F;
-    return cosf(x[i] * (float)(1 << f));
+  for (int k = 6 * F + q; k < width; k += 4) {
+    const int a = k - 6 * F;
+    float v = a == 0 ? x[0] : 0.0f;
+    v = a == 1 ? x[1] : v;
+    v = a == 2 ? x[2] : v;
+    v = append ? v : 0.0f;
+    act[lds_idx<T>(m, col0 + k)] = to_t<T>(v);
+    if (sv) sv[(int64_t)k * Npad] = to_t<T>(v);
   }
-  if (append && k < 6 * F + 3) return x[k - 6 * F];
-  return 0.0f;
+}
+
+// dot of `w[0..NK)` with LDS row m, columns [k0, k0 + NK) (k0 a multiple of the chunk width), summed in column order
+template <typename T> __device__ __forceinline__ void unpack_chunk(f4 raw, float (&v)[Cfg<T>::EPC]);
+template <> __device__ __forceinline__ void unpack_chunk<float>(f4 raw, float (&v)[4]) {
+  v[0] = raw.x; v[1] = raw.y; v[2] = raw.z; v[3] = raw.w;
+}
+template <> __device__ __forceinline__ void unpack_chunk<bf16_t>(f4 raw, float (&v)[8]) {
+  const uint32_t w[4] = {__float_as_uint(raw.x), __float_as_uint(raw.y), __float_as_uint(raw.z),
+                         __float_as_uint(raw.w)};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
 }
 
 __device__ __forceinline__ void store_mask_tile(uint64_t* masks, int64_t Npad, int slot, int64_t pt16, int ft, f4 v,
@@ -351,11 +457,9 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
   float x3[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) x3[i] = o3[i] + t * d3[i];  // models/utils.py:244
-  for (int k = 16 * q; k < 16 * q + 16; ++k) {
-    float v = (k < lay.xyz_dim) ? pe_value(x3, k, lay.fx, lay.ax) : 0.0f;
-    act[lds_idx<T>(mt_, PE_COL + k)] = to_t<T>(v);
-    if (saved) saved[(SR.pe + k) * Npad + p] = to_t<T>(v);
-  }
+  if (!(YANERF_ABLATE & 2))
+    harmonic_to_lds<T>(act, mt_, PE_COL, KPE, x3, lay.fx, lay.ax, q, saved ? saved + SR.pe * Npad + p : nullptr,
+                       Npad);
   __syncthreads();
 
   f4 acc[NT][MT];
@@ -378,7 +482,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
         v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         const int m = 16 * mt + li;
         lds_put4<T>(act, m, n, v);
-        if (saved) {
+        if (saved && !(YANERF_ABLATE & 4)) {
           T* s = saved + (SR.h0 + 256LL * l + n) * Npad + p0 + m;
           s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
           const int sh = (nt * MT + mt) * 4;
@@ -387,15 +491,27 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
         }
       }
     }
-    if (saved) masks[(((int64_t)l * gridDim.x + blockIdx.x) * WAVES + wave) * 64 + lane] = bits;
+    if (saved && !(YANERF_ABLATE & 4)) masks[(((int64_t)l * gridDim.x + blockIdx.x) * WAVES + wave) * 64 + lane] = bits;
     __syncthreads();
   }
   // ---- density head (VALU): sigma = w_d . h + b_d  (nerf_mlp.py:173; density_layer 256->1)
   float sig;
   {
-    const float* wd = Wf + lay.wd_off;
+    const float* wd = Wf + lay.wd_off + 64 * q;
     float s = 0.0f;
-    for (int k = 64 * q; k < 64 * q + 64; ++k) s += wd[k] * to_f<T>(act[lds_idx<T>(mt_, k)]);
+#pragma unroll 2
+    for (int c = 0; c < ((YANERF_ABLATE & 8) ? 0 : 64 / EPC); ++c) {
+      float v[EPC];
+      unpack_chunk<T>(lds_chunk<T>(act, mt_, (64 * q) / EPC + c), v);
+#pragma unroll
+      for (int e = 0; e < EPC; e += 4) {
+        const f4 w = *(const f4*)(wd + c * EPC + e);
+        s += w.x * v[e];
+        s += w.y * v[e + 1];
+        s += w.z * v[e + 2];
+        s += w.w * v[e + 3];
+      }
+    }
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     sig = s + Wf[lay.bd_off];
@@ -425,11 +541,9 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
   {
     const float nrm = fmaxf(sqrtf(d3[0] * d3[0] + d3[1] * d3[1] + d3[2] * d3[2]), 1e-12f);
     float dn[3] = {d3[0] / nrm, d3[1] / nrm, d3[2] / nrm};
-    for (int k = 8 * q; k < 8 * q + 8; ++k) {
-      float v = (k < lay.dir_dim) ? pe_value(dn, k, lay.fd, lay.ad) : 0.0f;
-      act[lds_idx<T>(mt_, PE_COL + k)] = to_t<T>(v);
-      if (saved) saved[(SR.dpe + k) * Npad + p] = to_t<T>(v);
-    }
+    if (!(YANERF_ABLATE & 2))
+      harmonic_to_lds<T>(act, mt_, PE_COL, KDIR, dn, lay.fd, lay.ad, q, saved ? saved + SR.dpe * Npad + p : nullptr,
+                         Npad);
   }
   __syncthreads();
   // ---- color layer: LinearWithRepeat(256 + 27 -> 128) + ReLU as one K = 288 GEMM over [Y, dirPE]
@@ -463,10 +577,22 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
   {
     const float* wo = Wf + lay.wo_off;
     float u[CMAX] = {0.f, 0.f, 0.f, 0.f};
-    for (int c = 32 * q; c < 32 * q + 32; ++c) {
-      float cv = to_f<T>(act[lds_idx<T>(mt_, c)]);
+    for (int c = 0; c < ((YANERF_ABLATE & 8) ? 0 : 32 / EPC); ++c) {
+      float v[EPC];
+      unpack_chunk<T>(lds_chunk<T>(act, mt_, (32 * q) / EPC + c), v);
 #pragma unroll
-      for (int j = 0; j < CMAX; ++j) u[j] += wo[j * HC + c] * cv;
+      for (int j = 0; j < CMAX; ++j) {
+        if (j < lay.cdim) {
+#pragma unroll
+          for (int e = 0; e < EPC; e += 4) {
+            const f4 w = *(const f4*)(wo + j * HC + 32 * q + c * EPC + e);
+            u[j] += w.x * v[e];
+            u[j] += w.y * v[e + 1];
+            u[j] += w.z * v[e + 2];
+            u[j] += w.w * v[e + 3];
+          }
+        }
+      }
     }
 #pragma unroll
     for (int j = 0; j < CMAX; ++j) {

@@ -862,11 +862,13 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int kt, int s, int S, in
 template <typename T>
 __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t Npad, int S, float* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) char smem[(256 + DW_BK) * 128];
-  const int tile = blockIdx.x, s = blockIdx.y;
+  // 1-D grid in job order (heaviest first); inside a job, split-major so the k-tiles sharing a dZ slab run together
+  const int b = blockIdx.x;
   int ji = 0;
-  while (ji + 1 < jobs.n && jobs.j[ji + 1].tile_base <= tile) ++ji;
+  while (ji + 1 < jobs.n && jobs.j[ji + 1].tile_base * S <= b) ++ji;
   const DwJob& J = jobs.j[ji];
-  const int kt = tile - J.tile_base;
+  const int local = b - J.tile_base * S;
+  const int s = local / J.k_tiles, kt = local % J.k_tiles;
   if (J.bn == 256) dw_tile<T, 256>(J, kt, s, S, Npad, slab, jobs.slab_elems, smem);
   else if (J.bn == 128) dw_tile<T, 128>(J, kt, s, S, Npad, slab, jobs.slab_elems, smem);
   else dw_tile<T, 64>(J, kt, s, S, Npad, slab, jobs.slab_elems, smem);
@@ -929,8 +931,9 @@ static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, const f
   return 0;
 }
 
+// point splits per dW tile: enough workgroups that the light jobs dispatched last fill the tail of the heavy ones
 static int dw_splits(int total_tiles, int64_t n_stages) {
-  int64_t S = (1024 + total_tiles - 1) / total_tiles;
+  int64_t S = (4096 + total_tiles - 1) / total_tiles;
   if (S > n_stages) S = n_stages;
   if (S > 64) S = 64;
   if (S < 1) S = 1;
@@ -951,10 +954,11 @@ static void for_each_dw_job(const MlpLayout& L, F&& f) {
     else if (sk) f(GR.dz0 + 256LL * l, nout, SR.h0 + 256LL * (l - 1), 256, SR.pe, L.xyz_dim, 2 * l);
     else f(GR.dz0 + 256LL * l, nout, SR.h0 + 256LL * (l - 1), 256, -1, 0, 2 * l);
   }
+  // heaviest jobs first: the grid is dispatched in job order, so the light ones fill the last round
   const int h = 2 * L.L;
   f(GR.dyx, L.hid, SR.h0 + 256LL * (L.L - 1), L.hid, -1, 0, h + 0);        // intermediate_linear
-  f(GR.dyx + 256, 1, SR.h0 + 256LL * (L.L - 1), L.hid, -1, 0, h + 2);      // density_layer
   f(GR.dzc, L.hdir, SR.y, L.hid, SR.dpe, L.dir_dim, h + 4);               // color_layer.0 (LinearWithRepeat)
+  f(GR.dyx + 256, 1, SR.h0 + 256LL * (L.L - 1), L.hid, -1, 0, h + 2);      // density_layer
   f(GR.du, L.cdim, SR.c, L.hdir, -1, 0, h + 6);                           // color_layer.2
 }
 
@@ -1026,8 +1030,7 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   DwJobs D;
   build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D);
   const int S = dw_splits(D.total_tiles, Npad / (2 * Cfg<T>::KB));
-  hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)D.total_tiles, (unsigned)S), dim3(DW_THREADS), 0, st, D, Npad, S,
-                     slab);
+  hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)(D.total_tiles * S)), dim3(DW_THREADS), 0, st, D, Npad, S, slab);
   YN_LAUNCH_CHECK("mlp_backward_dw");
   hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((D.slab_elems + 255) / 256)), dim3(256), 0, st, D, S, slab);
   YN_LAUNCH_CHECK("mlp_backward_reduce");

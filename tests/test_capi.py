@@ -62,10 +62,13 @@ def test_mlp_size_queries():
     f32 = L.yanerf_mlp_packed_bytes(ctypes.byref(d), _C.PREC_F32)
     bf = L.yanerf_mlp_packed_bytes(ctypes.byref(d), _C.PREC_BF16)
     assert f32 > bf > 0
-    # saved activations grow linearly with the point count (rounded up to the kernel's point tile)
+    # saved activations grow with the point count, rounded up to the kernel's point tile; rows are padded to an
+    # odd multiple of 256 B (HBM channel spread), so the size is ~linear, never below the unpadded bytes
     s1 = L.yanerf_mlp_saved_bytes(ctypes.byref(d), _C.PREC_F32, 64)
     s2 = L.yanerf_mlp_saved_bytes(ctypes.byref(d), _C.PREC_F32, 128)
-    assert s2 == 2 * s1 and L.yanerf_mlp_saved_bytes(ctypes.byref(d), _C.PREC_F32, 65) == s2
+    assert s1 < s2 and L.yanerf_mlp_saved_bytes(ctypes.byref(d), _C.PREC_F32, 65) == s2
+    rows = 64 + 256 * 8 + 256 + 32 + 128  # PE | 8 trunk layers | Y | dir PE | colour hidden
+    assert s2 >= rows * 128 * 4 + 9 * 128 * 32
     assert L.yanerf_mlp_bwd_workspace_bytes(ctypes.byref(d), _C.PREC_BF16, 1 << 20) > 0
 
 

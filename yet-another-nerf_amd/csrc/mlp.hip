@@ -28,14 +28,19 @@
 #ifndef YANERF_ABLATE
 #define YANERF_ABLATE 0
 #endif
+#ifndef YANERF_LOWREG
+#define YANERF_LOWREG 0
+#endif
 
 namespace yanerf {
 
 typedef unsigned short bf16_t;
 
 template <typename T> struct Cfg;
-template <> struct Cfg<float> { static constexpr int M = 64, WAVES = 4, EPC = 4, KB = 16, APREF = 1; };
-template <> struct Cfg<bf16_t> { static constexpr int M = 128, WAVES = 8, EPC = 8, KB = 32, APREF = 3; };
+template <> struct Cfg<float> { static constexpr int M = 64, WAVES = 4, EPC = 4, KB = 16, APREF = 1, LOWREG = 0, WPE = 2; };
+template <> struct Cfg<bf16_t> {
+  static constexpr int M = 128, WAVES = 8, EPC = 8, KB = 32, APREF = 3, LOWREG = YANERF_LOWREG, WPE = LOWREG ? 4 : 2;
+};
 
 constexpr int ROW = 320;    // LDS row length (elements)
 constexpr int PE_COL = 256; // xyz-PE / dir-PE column base
@@ -62,7 +67,7 @@ struct MlpLayout {
   int64_t bytes;
 };
 
-// saved activation rows (units of Npad elements of T)
+// saved activation rows (each row_ld(Npad) elements of T)
 struct SavedRows {
   int64_t pe, h0, y, dpe, c, rows;
 };
@@ -101,8 +106,16 @@ __host__ __device__ inline int64_t mask_words_per_slot(int64_t Npad) { return Np
 __device__ __forceinline__ int64_t mask_index(int64_t Npad, int slot, int64_t pt16, int ft) {
   return (((int64_t)slot * (Npad / 16) + pt16) * 16 + ft) * 4;
 }
+// Row stride of the feature-major saved / gradient buffers: Npad padded so a row is an ODD multiple of 256 B.
+// With Npad a multiple of large powers of two, equal points of consecutive rows would otherwise sit on the
+// same HBM channel, and a dW stage reading 384 rows at one point offset would hit that one channel.
+__host__ __device__ inline int64_t row_ld(int64_t Npad, size_t es) {
+  int64_t units = (Npad * (int64_t)es + 255) / 256;
+  if ((units & 1) == 0) ++units;
+  return units * 256 / (int64_t)es;
+}
 static int64_t saved_t_bytes(int L, int64_t Npad, size_t es) {
-  return (saved_rows(L).rows * Npad * (int64_t)es + 255) / 256 * 256;
+  return saved_rows(L).rows * row_ld(Npad, es) * (int64_t)es;
 }
 
 static int64_t tile_m(int prec) { return prec == YANERF_PREC_F32 ? Cfg<float>::M : Cfg<bf16_t>::M; }
@@ -250,7 +263,9 @@ template <> __device__ __forceinline__ f4 mma_blk<bf16_t>(f4 a, f4 b, f4 c) {
 // acc[i][j] += A_i x B_j over one 64-byte K-block for a grid of independent accumulators. fp32: the four
 // 16x16x4 k-steps are the OUTER loop so consecutive MFMAs never depend on each other (dependent-accumulator
 // latency 40 cycles > 32-cycle issue); bf16: one 16x16x32 per pair.
-template <typename T, int NI, int NJ>
+// SWAP: multiply b x a instead (the C tile comes out transposed: lane (g, li) holds column li of rows 4g..4g+3 of
+// the b side)
+template <typename T, int NI, int NJ, bool SWAP = false>
 __device__ __forceinline__ void mma_grid(const f4 (&a)[NI], const f4 (&b)[NJ], f4 (&acc)[NI][NJ]) {
   if constexpr (YANERF_ABLATE & 1) {
 #pragma unroll
@@ -266,12 +281,13 @@ __device__ __forceinline__ void mma_grid(const f4 (&a)[NI], const f4 (&b)[NJ], f
       for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+          acc[i][j] = SWAP ? __builtin_amdgcn_mfma_f32_16x16x4f32(b[j][s], a[i][s], acc[i][j], 0, 0, 0)
+                           : __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
   } else {
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = mma_blk<T>(a[i], b[j], acc[i][j]);
+      for (int j = 0; j < NJ; ++j) acc[i][j] = SWAP ? mma_blk<T>(b[j], a[i], acc[i][j]) : mma_blk<T>(a[i], b[j], acc[i][j]);
   }
 }
 
@@ -281,22 +297,47 @@ __device__ __forceinline__ void mma_grid(const f4 (&a)[NI], const f4 (&b)[NJ], f
 // stream through a register ring APREF K-blocks deep and the LDS fragments of block kb+1 are read while block kb
 // multiplies (the loop is unrolled by the ring depth so every ring slot is a static register set). Loads past the
 // last K-block re-read the last block (uniform, in-bounds, a few redundant L2 hits per layer).
+// bf16 weight-fragment ring (see gemm_lds). A caller may fill it for the NEXT GEMM before running the current
+// layer's epilogue, so that GEMM starts on weights already in registers instead of an L2 round trip.
+template <typename T, int NT> struct ARing { f4 a[Cfg<T>::APREF][NT]; };
+template <typename T, int NT>
+__device__ __forceinline__ void ring_fill(ARing<T, NT>& R, const T* __restrict__ W, int ldw, int nrow0, int nkb,
+                                          int lane) {
+  if constexpr (sizeof(T) == 2) {
+    constexpr int D = Cfg<T>::APREF, EPC = Cfg<T>::EPC, KB = Cfg<T>::KB, FRAG = 64 * EPC;
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      const int k = r < nkb ? r : nkb - 1;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        R.a[r][nt] = *(const f4*)(W + ((size_t)((nrow0 >> 4) + nt) * (ldw / KB) * 64 + lane) * EPC + k * FRAG);
+    }
+  }
+}
+
+// Accumulator layout: acc[nt][mt] lane (g, li) holds features nrow0 + 16nt + 4g .. +3 of point 16mt + li. The
+// accumulators start from the bias when one is given (the reference's addmm also accumulates onto the bias).
 template <typename T, int NT, int MT>
 __device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int nrow0, const T* act, int kc0, int nkb,
-                                         f4 (&acc)[NT][MT], int lane) {
+                                         f4 (&acc)[NT][MT], int lane, const float* __restrict__ bias = nullptr,
+                                         ARing<T, NT>* pre = nullptr) {
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
   const int g = lane >> 4, li = lane & 15;
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt)
+  for (int nt = 0; nt < NT; ++nt) {
+    const f4 b0 = bias ? *(const f4*)(bias + nrow0 + 16 * nt + 4 * g) : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = b0;
+  }
   // W is in A-fragment order (pack_kernel): row tile rt, K-block kb at ((rt * ldw / KB + kb) * 64 + lane) * EPC
   const T* wp[NT];
   constexpr int FRAG = 64 * EPC;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) wp[nt] = W + ((size_t)((nrow0 >> 4) + nt) * (ldw / KB) * 64 + lane) * EPC;
-  if constexpr (sizeof(T) == 2) {
-    constexpr int D = Cfg<T>::APREF;
+  if constexpr (sizeof(T) == 2 && Cfg<T>::LOWREG) {
+    // two workgroups per CU (<= 128 VGPRs): no LDS double buffer, a 2-deep weight ring; the other workgroup's
+    // waves cover the LDS / L2 latency
+    constexpr int D = 2;
     f4 a[D][NT];
 #pragma unroll
     for (int r = 0; r < D; ++r) {
@@ -304,6 +345,33 @@ __device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int n
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) a[r][nt] = *(const f4*)(wp[nt] + k * FRAG);
     }
+    auto step = [&](int kb, f4(&ar)[NT], bool refill) {
+      f4 bq[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) bq[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + kb * 4 + g);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[nt][mt] = mma_blk<T>(ar[nt], bq[mt], acc[nt][mt]);
+      if (refill) {
+        const int ka = kb + D < nkb ? kb + D : nkb - 1;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) ar[nt] = *(const f4*)(wp[nt] + ka * FRAG);
+      }
+    };
+    int kb = 0;
+    for (; kb + D <= nkb; kb += D) {
+#pragma unroll
+      for (int r = 0; r < D; ++r) step(kb + r, a[r], true);
+    }
+    if (kb < nkb) step(kb, a[0], false);
+    return;
+  }
+  if constexpr (sizeof(T) == 2) {
+    constexpr int D = Cfg<T>::APREF;
+    ARing<T, NT> own;
+    if (!pre) ring_fill<T, NT>(own, W, ldw, nrow0, nkb, lane);
+    f4(&a)[D][NT] = pre ? pre->a : own.a;
     f4 b[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) b[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + g);
@@ -352,23 +420,93 @@ __device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int n
   }
 }
 
-// write 4 consecutive features (rows n..n+3) of point m into the LDS tile
-template <typename T> __device__ __forceinline__ void lds_put4(T* act, int m, int n, f4 v);
-template <> __device__ __forceinline__ void lds_put4<float>(float* act, int m, int n, f4 v) {
-  *(f4*)(act + m * ROW + swz<float>(m, n / 4) * 4) = v;
+// ---- epilogue helpers on a "packed tile": features n..n+3 of one point (one accumulator lane) in storage form.
+// fp32: the f4 itself; bf16: two u32 words (x | y << 16, z | w << 16) from two v_cvt_pk_bf16_f32.
+// ReLU is an integer max with 0 on the stored bits (negative floats / bf16 are negative integers, +0 stays 0),
+// which avoids the IEEE canonicalisation a float max needs, and for bf16 runs on both halves at once.
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bh2 __attribute__((ext_vector_type(2)));
+typedef short s2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+template <typename T> struct Pk;
+template <> struct Pk<float> { f4 v; };
+template <> struct Pk<bf16_t> { uint32_t w0, w1; };
+
+template <typename T> __device__ __forceinline__ Pk<T> pk_make(f4 v);
+template <> __device__ __forceinline__ Pk<float> pk_make<float>(f4 v) { return Pk<float>{v}; }
+template <> __device__ __forceinline__ Pk<bf16_t> pk_make<bf16_t>(f4 v) {
+  const bh2 lo = __builtin_convertvector(f2{v.x, v.y}, bh2), hi = __builtin_convertvector(f2{v.z, v.w}, bh2);
+  return Pk<bf16_t>{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
 }
-template <> __device__ __forceinline__ void lds_put4<bf16_t>(bf16_t* act, int m, int n, f4 v) {
-  us4 h = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
-  *(us4*)(act + m * ROW + swz<bf16_t>(m, n / 8) * 8 + (n & 7)) = h;
+template <typename T> __device__ __forceinline__ Pk<T> pk_relu(Pk<T> p);
+template <> __device__ __forceinline__ Pk<float> pk_relu<float>(Pk<float> p) {
+  f4 r;
+  r.x = __int_as_float(max(__float_as_int(p.v.x), 0));
+  r.y = __int_as_float(max(__float_as_int(p.v.y), 0));
+  r.z = __int_as_float(max(__float_as_int(p.v.z), 0));
+  r.w = __int_as_float(max(__float_as_int(p.v.w), 0));
+  return Pk<float>{r};
+}
+template <> __device__ __forceinline__ Pk<bf16_t> pk_relu<bf16_t>(Pk<bf16_t> p) {
+  const s2 z = {0, 0};
+  return Pk<bf16_t>{__builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s2, p.w0), z)),
+                    __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s2, p.w1), z))};
+}
+// 4-bit ReLU mask of a relu'd packed tile: bit r = element r > 0
+template <typename T> __device__ __forceinline__ uint32_t pk_bits(Pk<T> p);
+template <> __device__ __forceinline__ uint32_t pk_bits<float>(Pk<float> p) {
+  const uint32_t b0 = min(__float_as_uint(p.v.x), 1u), b1 = min(__float_as_uint(p.v.y), 1u),
+                 b2 = min(__float_as_uint(p.v.z), 1u), b3 = min(__float_as_uint(p.v.w), 1u);
+  return b0 | (b1 << 1) | (b2 << 2) | (b3 << 3);
+}
+template <> __device__ __forceinline__ uint32_t pk_bits<bf16_t>(Pk<bf16_t> p) {
+  const u2 one = {1, 1};
+  const uint32_t m0 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u2, p.w0), one));
+  const uint32_t m1 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u2, p.w1), one));
+  const uint32_t t = m0 | (m1 << 2);  // x@0 z@2 y@16 w@18
+  return (t & 5u) | ((t >> 15) & 10u);
+}
+// write the packed tile to LDS row m, features n..n+3
+template <typename T> __device__ __forceinline__ void pk_lds(T* act, int m, int n, Pk<T> p);
+template <> __device__ __forceinline__ void pk_lds<float>(float* act, int m, int n, Pk<float> p) {
+  *(f4*)(act + m * ROW + swz<float>(m, n / 4) * 4) = p.v;
+}
+template <> __device__ __forceinline__ void pk_lds<bf16_t>(bf16_t* act, int m, int n, Pk<bf16_t> p) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  *(u32x2*)(act + m * ROW + swz<bf16_t>(m, n / 8) * 8 + (n & 7)) = u32x2{p.w0, p.w1};
+}
+// store the packed tile into 4 consecutive feature-major rows (stride ld)
+template <typename T> __device__ __forceinline__ void pk_store_rows(T* dst, int64_t ld, Pk<T> p);
+template <> __device__ __forceinline__ void pk_store_rows<float>(float* dst, int64_t ld, Pk<float> p) {
+  dst[0] = p.v.x;
+  dst[ld] = p.v.y;
+  dst[2 * ld] = p.v.z;
+  dst[3 * ld] = p.v.w;
+}
+template <> __device__ __forceinline__ void pk_store_rows<bf16_t>(bf16_t* dst, int64_t ld, Pk<bf16_t> p) {
+  dst[0] = (bf16_t)p.w0;
+  dst[ld] = (bf16_t)(p.w0 >> 16);
+  dst[2 * ld] = (bf16_t)p.w1;
+  dst[3 * ld] = (bf16_t)(p.w1 >> 16);
+}
+// zero the elements of v whose bit (bits >> sh .. sh+3) is clear
+__device__ __forceinline__ f4 apply_mask4(f4 v, uint64_t bits, int sh) {
+  const uint32_t w = (uint32_t)(bits >> sh);
+  f4 r;
+  r.x = __int_as_float(__float_as_int(v.x) & __builtin_amdgcn_sbfe(w, 0, 1));
+  r.y = __int_as_float(__float_as_int(v.y) & __builtin_amdgcn_sbfe(w, 1, 1));
+  r.z = __int_as_float(__float_as_int(v.z) & __builtin_amdgcn_sbfe(w, 2, 1));
+  r.w = __int_as_float(__float_as_int(v.w) & __builtin_amdgcn_sbfe(w, 3, 1));
+  return r;
 }
 
 // Harmonic embedding (models/utils.py:98-102) of 3-vector x: columns [sin(x_i 2^f) i-major f-minor | cos(...) | x],
 // zero-padded to `width`, written into LDS row m at column col0 (and, when `sv` is set, into feature-major saved
-// rows sv[k * Npad]). The 4 threads of a point share the work: thread q takes the (i, f) pairs j = q, q+4, ...
+// rows sv[k * ld]). The 4 threads of a point share the work: thread q takes the (i, f) pairs j = q, q+4, ...
 // and one sincosf per pair yields both the sin column j and the cos column 3F + j.
 template <typename T>
 __device__ __forceinline__ void harmonic_to_lds(T* act, int m, int col0, int width, const float x[3], int F,
-                                                int append, int q, T* sv, int64_t Npad) {
+                                                int append, int q, T* sv, int64_t ld) {
   for (int j = q; j < 3 * F; j += 4) {
     const int i = j / F, f = j - i * F;
     float xi = x[0];
@@ -388,8 +526,8 @@ __device__ __forceinline__ void harmonic_to_lds(T* act, int m, int col0, int wid
     act[lds_idx<T>(m, col0 + j)] = to_t<T>(sn);
     act[lds_idx<T>(m, col0 + 3 * F + j)] = to_t<T>(cs);
     if (sv) {
-      sv[(int64_t)j * Npad] = to_t<T>(sn);
-      sv[(int64_t)(3 * F + j) * Npad] = to_t<T>(cs);
+      sv[(int64_t)j * ld] = to_t<T>(sn);
+      sv[(int64_t)(3 * F + j) * ld] = to_t<T>(cs);
     }
   }
   for (int k = 6 * F + q; k < width; k += 4) {
@@ -399,7 +537,7 @@ __device__ __forceinline__ void harmonic_to_lds(T* act, int m, int col0, int wid
     v = a == 2 ? x[2] : v;
     v = append ? v : 0.0f;
     act[lds_idx<T>(m, col0 + k)] = to_t<T>(v);
-    if (sv) sv[(int64_t)k * Npad] = to_t<T>(v);
+    if (sv) sv[(int64_t)k * ld] = to_t<T>(v);
   }
 }
 
@@ -427,7 +565,7 @@ __device__ __forceinline__ void store_mask_tile(uint64_t* masks, int64_t Npad, i
 
 // ============================================================================================ forward
 template <typename T>
-__global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
+__global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_fwd_kernel(
     MlpLayout lay, const T* __restrict__ Wt, const float* __restrict__ Wf, const float* __restrict__ origins,
     const float* __restrict__ dirs, const float* __restrict__ lengths, int64_t R, int64_t P,
     float* __restrict__ sigma, float* __restrict__ rgb, T* __restrict__ saved, uint64_t* __restrict__ masks,
@@ -442,6 +580,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
   const int g = lane >> 4, li = lane & 15;
   const int64_t N = R * P;
   const int64_t p0 = (int64_t)blockIdx.x * M;
+  const int64_t ld = row_ld(Npad, sizeof(T));
   const SavedRows SR = saved_rows(lay.L);
   const int mt_ = tid >> 2, q = tid & 3;
   const int64_t p = p0 + mt_;
@@ -458,36 +597,35 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
 #pragma unroll
   for (int i = 0; i < 3; ++i) x3[i] = o3[i] + t * d3[i];  // models/utils.py:244
   if (!(YANERF_ABLATE & 2))
-    harmonic_to_lds<T>(act, mt_, PE_COL, KPE, x3, lay.fx, lay.ax, q, saved ? saved + SR.pe * Npad + p : nullptr,
-                       Npad);
+    harmonic_to_lds<T>(act, mt_, PE_COL, KPE, x3, lay.fx, lay.ax, q, saved ? saved + SR.pe * ld + p : nullptr,
+                       ld);
   __syncthreads();
 
   f4 acc[NT][MT];
   const int nrow0 = wave * NT * 16;
+  // weight ring of the next GEMM, filled before the current layer's epilogue (bf16; no-op for fp32)
+  ARing<T, NT> ring;
+  ring_fill<T, NT>(ring, Wt + lay.w_off[0], lay.kpad[0], nrow0, KPE / KB, lane);
   for (int l = 0; l < lay.L; ++l) {
     const bool sk = (lay.skip >> l) & 1u;
     const int kc0 = (l == 0) ? PE_COL / EPC : 0;
     const int nkb = (l == 0) ? KPE / KB : (sk ? 320 / KB : 256 / KB);
-    gemm_lds<T, NT, MT>(Wt + lay.w_off[l], lay.kpad[l], nrow0, act, kc0, nkb, acc, lane);
+    gemm_lds<T, NT, MT>(Wt + lay.w_off[l], lay.kpad[l], nrow0, act, kc0, nkb, acc, lane, Wf + lay.b_off[l], &ring);
+    if (l + 1 < lay.L) ring_fill<T, NT>(ring, Wt + lay.w_off[l + 1], lay.kpad[l + 1], nrow0, lay.kpad[l + 1] / KB, lane);
+    else ring_fill<T, NT>(ring, Wt + lay.wint_off, 256, nrow0, 256 / KB, lane);
     __syncthreads();
-    const float* bias = Wf + lay.b_off[l];
     uint64_t bits = 0;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int n = nrow0 + 16 * nt + 4 * g;
-      const f4 bv = *(const f4*)(bias + n);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        f4 v = acc[nt][mt] + bv;
-        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        const Pk<T> h = pk_relu<T>(pk_make<T>(acc[nt][mt]));
         const int m = 16 * mt + li;
-        lds_put4<T>(act, m, n, v);
+        pk_lds<T>(act, m, n, h);
         if (saved && !(YANERF_ABLATE & 4)) {
-          T* s = saved + (SR.h0 + 256LL * l + n) * Npad + p0 + m;
-          s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
-          const int sh = (nt * MT + mt) * 4;
-          bits |= ((uint64_t)(v.x > 0.f) << sh) | ((uint64_t)(v.y > 0.f) << (sh + 1)) |
-                  ((uint64_t)(v.z > 0.f) << (sh + 2)) | ((uint64_t)(v.w > 0.f) << (sh + 3));
+          pk_store_rows<T>(saved + (SR.h0 + 256LL * l + n) * ld + p0 + m, ld, h);
+          bits |= (uint64_t)pk_bits<T>(h) << ((nt * MT + mt) * 4);
         }
       }
     }
@@ -517,23 +655,22 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
     sig = s + Wf[lay.bd_off];
   }
   // ---- intermediate_linear (no activation)
-  gemm_lds<T, NT, MT>(Wt + lay.wint_off, 256, nrow0, act, 0, 256 / KB, acc, lane);
+  gemm_lds<T, NT, MT>(Wt + lay.wint_off, 256, nrow0, act, 0, 256 / KB, acc, lane, Wf + lay.bint_off, &ring);
+  const int crow0 = wave * NTC * 16;
+  ARing<T, NTC> ringc;
+  ring_fill<T, NTC>(ringc, Wt + lay.wc_off, KC, crow0, KC / KB, lane);
   __syncthreads();
   {
-    const float* bias = Wf + lay.bint_off;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int n = nrow0 + 16 * nt + 4 * g;
-      const f4 bv = *(const f4*)(bias + n);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        f4 v = acc[nt][mt] + bv;
+        f4 v = acc[nt][mt];
         const int m = 16 * mt + li;
-        lds_put4<T>(act, m, n, v);
-        if (saved) {
-          T* s = saved + (SR.y + n) * Npad + p0 + m;
-          s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
-        }
+        const Pk<T> h = pk_make<T>(v);
+        pk_lds<T>(act, m, n, h);
+        if (saved) pk_store_rows<T>(saved + (SR.y + n) * ld + p0 + m, ld, h);
       }
     }
   }
@@ -542,30 +679,27 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
     const float nrm = fmaxf(sqrtf(d3[0] * d3[0] + d3[1] * d3[1] + d3[2] * d3[2]), 1e-12f);
     float dn[3] = {d3[0] / nrm, d3[1] / nrm, d3[2] / nrm};
     if (!(YANERF_ABLATE & 2))
-      harmonic_to_lds<T>(act, mt_, PE_COL, KDIR, dn, lay.fd, lay.ad, q, saved ? saved + SR.dpe * Npad + p : nullptr,
-                         Npad);
+      harmonic_to_lds<T>(act, mt_, PE_COL, KDIR, dn, lay.fd, lay.ad, q, saved ? saved + SR.dpe * ld + p : nullptr,
+                         ld);
   }
   __syncthreads();
   // ---- color layer: LinearWithRepeat(256 + 27 -> 128) + ReLU as one K = 288 GEMM over [Y, dirPE]
   {
     f4 accc[NTC][MT];
-    const int crow0 = wave * NTC * 16;
-    gemm_lds<T, NTC, MT>(Wt + lay.wc_off, KC, crow0, act, 0, KC / KB, accc, lane);
+    gemm_lds<T, NTC, MT>(Wt + lay.wc_off, KC, crow0, act, 0, KC / KB, accc, lane, Wf + lay.bc_off, &ringc);
     __syncthreads();
-    const float* bias = Wf + lay.bc_off;
 #pragma unroll
     for (int nt = 0; nt < NTC; ++nt) {
       const int n = crow0 + 16 * nt + 4 * g;
-      const f4 bv = *(const f4*)(bias + n);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        f4 v = accc[nt][mt] + bv;
+        f4 v = accc[nt][mt];
         v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         const int m = 16 * mt + li;
-        lds_put4<T>(act, m, n, v);
+        const Pk<T> h = pk_make<T>(v);
+        pk_lds<T>(act, m, n, h);
         if (saved) {
-          T* s = saved + (SR.c + n) * Npad + p0 + m;
-          s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
+          pk_store_rows<T>(saved + (SR.c + n) * ld + p0 + m, ld, h);
           store_mask_tile(masks + (int64_t)lay.L * mask_words_per_slot(Npad), Npad, 0, p0 / 16 + mt,
                           (crow0 + 16 * nt) / 16, v, lane);
         }
@@ -611,7 +745,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_fwd_kernel(
 
 // ============================================================================================ backward dX
 template <typename T>
-__global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
+__global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_bwd_dx_kernel(
     MlpLayout lay, const T* __restrict__ Wt, const float* __restrict__ Wf, const T* __restrict__ saved,
     const uint64_t* __restrict__ masks, const float* __restrict__ rgb, const float* __restrict__ g_sigma,
     const float* __restrict__ g_rgb, int64_t N, int64_t Npad, T* __restrict__ grad) {
@@ -623,6 +757,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int64_t p0 = (int64_t)blockIdx.x * M;
+  const int64_t ld = row_ld(Npad, sizeof(T));
   const GradRows GR = grad_rows(lay.L);
   const int mt_ = tid >> 2, q = tid & 3;
   const int64_t p = p0 + mt_;
@@ -638,8 +773,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
     }
   }
   if (q == 0) {
-    for (int j = 0; j < cd; ++j) grad[(GR.du + j) * Npad + p] = to_t<T>(du[j]);
-    grad[(GR.dyx + 256) * Npad + p] = to_t<T>(gs);
+    for (int j = 0; j < cd; ++j) grad[(GR.du + j) * ld + p] = to_t<T>(du[j]);
+    grad[(GR.dyx + 256) * ld + p] = to_t<T>(gs);
   }
   {
     const float* wo = Wf + lay.wo_off;
@@ -653,12 +788,12 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
     for (int c = 32 * q; c < 32 * q + 32; ++c) {
       float dc = 0.0f;
       for (int j = 0; j < cd; ++j) dc += du[j] * wo[j * HC + c];
-      const int cl = c & 15;
+      const int cl = c & 15;  // feature within its 16-feature tile: ballot word cl & 3, bit 16 * (cl >> 2) + point
       const uint64_t word = cw[(c >> 4) & 1][cl & 3];
       const bool on = (word >> (16 * (cl >> 2) + (mt_ & 15))) & 1ull;
       float dz = on ? dc : 0.0f;
       act[lds_idx<T>(mt_, c)] = to_t<T>(dz);
-      grad[(GR.dzc + c) * Npad + p] = to_t<T>(dz);
+      grad[(GR.dzc + c) * ld + p] = to_t<T>(dz);
     }
   }
   __syncthreads();
@@ -666,6 +801,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
   const int nrow0 = wave * NT * 16;
   // ---- dY = Wc[:, :256]^T dZc   (K = 128)
   gemm_lds<T, NT, MT>(Wt + lay.wcT_off, HC, nrow0, act, 0, HC / KB, acc, lane);
+  ARing<T, NT> ring;  // next GEMM's weights, fetched during the epilogue (bf16)
+  ring_fill<T, NT>(ring, Wt + lay.wintT_off, 256, nrow0, 256 / KB, lane);
   __syncthreads();
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
@@ -674,9 +811,9 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
     for (int mt = 0; mt < MT; ++mt) {
       const int m = 16 * mt + li;
       f4 v = acc[nt][mt];
-      lds_put4<T>(act, m, n, v);
-      T* s = grad + (GR.dyx + n) * Npad + p0 + m;
-      s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
+      const Pk<T> h = pk_make<T>(v);
+      pk_lds<T>(act, m, n, h);
+      pk_store_rows<T>(grad + (GR.dyx + n) * ld + p0 + m, ld, h);
     }
   }
   __syncthreads();
@@ -686,7 +823,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
     const T* A = (l == lay.L) ? Wt + lay.wintT_off : Wt + lay.wt_off[l];
     const int hl = l - 1;  // layer whose output gradient we form
     const uint64_t bits = masks[(((int64_t)hl * gridDim.x + blockIdx.x) * WAVES + wave) * 64 + lane];
-    gemm_lds<T, NT, MT>(A, 256, nrow0, act, 0, 256 / KB, acc, lane);
+    gemm_lds<T, NT, MT>(A, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring);
+    if (l - 1 >= 1) ring_fill<T, NT>(ring, Wt + lay.wt_off[l - 1], 256, nrow0, 256 / KB, lane);
     __syncthreads();
     const float* wd = Wf + lay.wd_off;
 #pragma unroll
@@ -702,14 +840,9 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
           v = v + wdv * gsm;
         }
         // ReLU mask of H_{hl}: this lane's own bits of this tile (packed by the forward)
-        const int sh = (nt * MT + mt) * 4;
-        v.x = ((bits >> sh) & 1ull) ? v.x : 0.f;
-        v.y = ((bits >> (sh + 1)) & 1ull) ? v.y : 0.f;
-        v.z = ((bits >> (sh + 2)) & 1ull) ? v.z : 0.f;
-        v.w = ((bits >> (sh + 3)) & 1ull) ? v.w : 0.f;
-        lds_put4<T>(act, m, n, v);
-        T* s = grad + (GR.dz0 + 256LL * hl + n) * Npad + p0 + m;
-        s[0] = to_t<T>(v.x); s[Npad] = to_t<T>(v.y); s[2 * Npad] = to_t<T>(v.z); s[3 * Npad] = to_t<T>(v.w);
+        const Pk<T> h = pk_make<T>(apply_mask4(v, bits, (nt * MT + mt) * 4));
+        pk_lds<T>(act, m, n, h);
+        pk_store_rows<T>(grad + (GR.dz0 + 256LL * hl + n) * ld + p0 + m, ld, h);
       }
     }
     __syncthreads();
@@ -726,7 +859,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) mlp_bwd_dx_kernel(
 // rows in the k-tile-0 workgroups. Partial tiles go to per-split fp32 slabs; dw_reduce sums them in split
 // order (deterministic) straight into the reference-layout gradient tensors.
 struct DwJob {
-  const void* A;  // dZ rows [a_rows][Npad]
+  const void* A;  // dZ rows [a_rows][ld] (points contiguous)
   int a_rows;
   const void* X0;  // layer input rows: segment 0 then segment 1
   int x0_rows;
@@ -751,72 +884,83 @@ constexpr int DW_BK = 128, DW_THREADS = 512;
 template <typename T> __device__ __forceinline__ float hsum16(f4 v);
 template <> __device__ __forceinline__ float hsum16<float>(f4 v) { return (v.x + v.y) + (v.z + v.w); }
 template <> __device__ __forceinline__ float hsum16<bf16_t>(f4 v) {
-  us8 h = __builtin_bit_cast(us8, v);
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  const bf2 one = __builtin_bit_cast(bf2, 0x3f803f80u);
   float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) s += bf2f(h[i]);
+  s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, v.x), one, s, false);
+  s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, v.y), one, s, false);
+  s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, v.z), one, s, false);
+  s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, v.w), one, s, false);
   return s;
 }
+
+// Stage ring: DW_STAGES buffers of up to (256 + DW_BK) rows x 128 B, filled by LDS-DMA (global_load_lds_dwordx4,
+// one wave-instruction = 8 whole rows) two stages ahead of the one being multiplied. The DMA destination is
+// lane-linear, so the XOR swizzle goes on the SOURCE chunk. One raw barrier per stage: after it every wave's DMA
+// for this stage has landed (each wave waited for its own with a counted vmcnt) and every wave is done reading
+// the buffer the next DMA overwrites.
+constexpr int DW_STAGES = 3, DW_STAGE_BYTES = (256 + DW_BK) * 128;
 
 template <typename T, int BN>
 __device__ __forceinline__ void dw_tile(const DwJob& J, int kt, int s, int S, int64_t Npad, float* __restrict__ slab,
                                         int64_t slab_elems, char* smem) {
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
   constexpr int WN = BN / 64, WK = 8 / WN, WKW = DW_BK / WK, KTW = WKW / 16;
-  constexpr int ROWS = BN + DW_BK, PER = ROWS * 8 / DW_THREADS;
-  static_assert(ROWS * 8 % DW_THREADS == 0, "staging split");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int ROWS = BN + DW_BK, PW = ROWS / 64;  // DMA wave-instructions per wave per stage
+  static_assert(ROWS % 64 == 0, "staging split");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int wn = wave / WK, wk = wave % WK;
   const int k0 = kt * DW_BK;
   constexpr int SPTS = 2 * KB;  // points per stage (128 B per row)
-  const int64_t nst = Npad / SPTS;
+  const int64_t nst = Npad / SPTS, ld = row_ld(Npad, sizeof(T));
   const int64_t st_lo = nst * s / S, st_hi = nst * (s + 1) / S;
-  const T* src[PER];
-  int lrow[PER], lch[PER];
+  // this lane's DMA source rows: wave-instruction i covers rows 8 * (wave * PW + i) .. + 8, lane -> (row, slot)
+  const T* src[PW];
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int idx = tid + DW_THREADS * i;
-    const int row = idx >> 3, ch = idx & 7;
-    lrow[i] = row;
-    lch[i] = ch;
-    const T* p = nullptr;
+  for (int i = 0; i < PW; ++i) {
+    const int row = 8 * (wave * PW + i) + (lane >> 3);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    const T* p;
     if (row < BN) {
-      if (row < J.a_rows) p = (const T*)J.A + (int64_t)row * Npad;
+      p = (const T*)J.A + (int64_t)(row < J.a_rows ? row : 0) * ld;  // rows past a_rows: any valid row (unused)
     } else {
       const int k = k0 + row - BN;
-      if (k < J.x0_rows) p = (const T*)J.X0 + (int64_t)k * Npad;
-      else if (k < J.x0_rows + J.x1_rows) p = (const T*)J.X1 + (int64_t)(k - J.x0_rows) * Npad;
+      if (k < J.x0_rows) p = (const T*)J.X0 + (int64_t)k * ld;
+      else if (k < J.ktot) p = (const T*)J.X1 + (int64_t)(k - J.x0_rows) * ld;
+      else p = (const T*)J.X0;  // columns past ktot are never stored
     }
-    src[i] = p ? p + ch * EPC : nullptr;
+    src[i] = p + ch * EPC;
   }
-  const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
-  f4 regs[PER];
-  float rsum[PER];
+  auto issue = [&](int64_t st) {
+    char* dst = smem + (int)(st % DW_STAGES) * DW_STAGE_BYTES + wave * PW * 1024;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) rsum[i] = 0.f;
+    for (int i = 0; i < PW; ++i)
+      __builtin_amdgcn_global_load_lds(src[i] + st * SPTS, (__attribute__((address_space(3))) void*)(dst + i * 1024),
+                                       16, 0, 0);
+  };
+  const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
+  constexpr int BPT = BN * 8 / DW_THREADS > 0 ? BN * 8 / DW_THREADS : 1;  // bias chunks per thread
+  float rsum[BPT];
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) rsum[i] = 0.f;
   const bool do_bias = (kt == 0);
   f4 acc[4][KTW];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
     for (int q = 0; q < KTW; ++q) acc[nt][q] = zero;
-  if (st_lo < st_hi) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) regs[i] = src[i] ? *(const f4*)(src[i] + st_lo * SPTS) : zero;
-  }
+  if (st_lo < st_hi) issue(st_lo);
+  if (st_lo + 1 < st_hi) issue(st_lo + 1);
   for (int64_t st = st_lo; st < st_hi; ++st) {
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      *(f4*)(smem + lrow[i] * 128 + ((lch[i] ^ ((lrow[i] >> 1) & 7)) << 4)) = regs[i];
-      if (do_bias && lrow[i] < BN) rsum[i] += hsum16<T>(regs[i]);
-    }
-    __syncthreads();
-    if (st + 1 < st_hi) {
-#pragma unroll
-      for (int i = 0; i < PER; ++i) regs[i] = src[i] ? *(const f4*)(src[i] + (st + 1) * SPTS) : zero;
-    }
+    // my DMA for stage st is complete once at most the next stage's PW remain outstanding
+    if (st + 1 < st_hi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (st + 2 < st_hi) issue(st + 2);
+    const char* buf = smem + (int)(st % DW_STAGES) * DW_STAGE_BYTES;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
       const int c = kb * 4 + g;
@@ -824,14 +968,21 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int kt, int s, int S, in
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
         const int row = wn * 64 + 16 * nt + li;
-        a[nt] = *(const f4*)(smem + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+        a[nt] = *(const f4*)(buf + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
       }
 #pragma unroll
       for (int q = 0; q < KTW; ++q) {
         const int row = BN + wk * WKW + 16 * q + li;
-        b[q] = *(const f4*)(smem + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+        b[q] = *(const f4*)(buf + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
       }
       mma_grid<T, 4, KTW>(a, b, acc);
+    }
+    if (do_bias) {
+#pragma unroll
+      for (int i = 0; i < BPT; ++i) {
+        const int idx = tid + DW_THREADS * i, row = idx >> 3, ch = idx & 7;
+        if (row < BN) rsum[i] += hsum16<T>(*(const f4*)(buf + row * 128 + (ch << 4)));
+      }
     }
   }
   float* out = slab + (int64_t)s * slab_elems + J.slab_off;
@@ -849,19 +1000,20 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int kt, int s, int S, in
     }
   if (do_bias) {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
+    for (int i = 0; i < BPT; ++i) {
+      const int idx = tid + DW_THREADS * i, row = idx >> 3;
       float v = rsum[i];
       v += __shfl_xor(v, 1, 64);
       v += __shfl_xor(v, 2, 64);
       v += __shfl_xor(v, 4, 64);
-      if (lch[i] == 0 && lrow[i] < BN && lrow[i] < J.a_rows) out[(int64_t)lrow[i] * kv + J.ktot] = v;
+      if ((idx & 7) == 0 && row < BN && row < J.a_rows) out[(int64_t)row * kv + J.ktot] = v;
     }
   }
 }
 
 template <typename T>
 __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t Npad, int S, float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) char smem[(256 + DW_BK) * 128];
+  __shared__ __attribute__((aligned(16))) char smem[DW_STAGES * DW_STAGE_BYTES];
   // 1-D grid in job order (heaviest first); inside a job, split-major so the k-tiles sharing a dZ slab run together
   const int b = blockIdx.x;
   int ji = 0;
@@ -965,8 +1117,9 @@ static void for_each_dw_job(const MlpLayout& L, F&& f) {
 static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void* gradbuf, int64_t Npad,
                           float* const* grads, DwJobs& D) {
   const size_t es = elem_size(prec);
-  auto srow = [&](int64_t r) { return r < 0 ? nullptr : (const void*)((const char*)saved + r * Npad * es); };
-  auto grow = [&](int64_t r) { return (const void*)((const char*)gradbuf + r * Npad * es); };
+  const int64_t ld = row_ld(Npad, es);
+  auto srow = [&](int64_t r) { return r < 0 ? nullptr : (const void*)((const char*)saved + r * ld * es); };
+  auto grow = [&](int64_t r) { return (const void*)((const char*)gradbuf + r * ld * es); };
   D.n = 0;
   D.total_tiles = 0;
   D.slab_elems = 0;
@@ -1021,7 +1174,7 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   const float* Wf = (const float*)((const char*)packed + L.f_base);
   const GradRows GR = grad_rows(L.L);
   T* gradbuf = (T*)ws;
-  int64_t grad_bytes = (GR.rows * Npad * (int64_t)sizeof(T) + 255) / 256 * 256;
+  int64_t grad_bytes = GR.rows * row_ld(Npad, sizeof(T)) * (int64_t)sizeof(T);
   float* slab = (float*)((char*)ws + grad_bytes);
   const uint64_t* masks = (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(T)));
   hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::WAVES * 64), 0, st, L, Wt,
@@ -1083,7 +1236,7 @@ int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, 
   MlpLayout L = make_layout(d, precision);
   const int64_t Npad = npad_of(precision, n_points);
   const GradRows GR = grad_rows(d->n_layers);
-  int64_t grad_bytes = (GR.rows * Npad * (int64_t)elem_size(precision) + 255) / 256 * 256;
+  int64_t grad_bytes = GR.rows * row_ld(Npad, elem_size(precision)) * (int64_t)elem_size(precision);
   int tiles = 0;
   int64_t se = dw_slab_elems_for(L, &tiles);
   const int64_t kb = precision == YANERF_PREC_F32 ? Cfg<float>::KB : Cfg<bf16_t>::KB;

@@ -24,7 +24,7 @@
 #include "common.hpp"
 
 // Development-only timing ablations (never set in the product build): 1 = no MFMA, 2 = no harmonic embedding,
-// 4 = no bias/ReLU/saved stores in the trunk epilogue, 8 = no VALU heads.
+// 4 = no saved stores in the trunk epilogue, 8 = no VALU heads, 16 = no trunk LDS writes, 32 = no trunk barriers.
 #ifndef YANERF_ABLATE
 #define YANERF_ABLATE 0
 #endif
@@ -59,6 +59,7 @@ struct MlpLayout {
   int kpad[MAXL];
   int64_t wt_off[MAXL];
   int64_t wint_off, wintT_off, wc_off, wcT_off;
+  int64_t wdh_off, woh_off;  // density / colour-output heads as 16-row GEMM operands (rows past 1 / cdim are 0)
   int64_t t_elems;
   int64_t f_base;  // byte offset of the fp32 section
   int64_t b_off[MAXL];
@@ -164,6 +165,8 @@ static MlpLayout make_layout(const yanerf_mlp_desc* d, int prec) {
   L.wintT_off = t; t += 256LL * 256;
   L.wc_off = t; t += (int64_t)HC * KC;
   L.wcT_off = t; t += 256LL * HC;
+  L.wdh_off = t; t += 16LL * 256;
+  L.woh_off = t; t += 16LL * HC;
   L.t_elems = t;
   int64_t tb = t * (int64_t)elem_size(prec);
   L.f_base = (tb + 255) / 256 * 256;
@@ -507,22 +510,44 @@ __device__ __forceinline__ f4 apply_mask4(f4 v, uint64_t bits, int sh) {
 template <typename T>
 __device__ __forceinline__ void harmonic_to_lds(T* act, int m, int col0, int width, const float x[3], int F,
                                                 int append, int q, T* sv, int64_t ld) {
+  if constexpr (sizeof(T) == 2) {
+    // bf16 mode: thread q < 3 takes coordinate q at every frequency with the hardware sin/cos of the angle
+    // reduced to revolutions (|error| ~1e-4 rad at the top frequency, far below the bf16 rounding of the value);
+    // thread 3 writes [x, zero padding]
+    if (q < 3) {
+      const float xi = q == 0 ? x[0] : (q == 1 ? x[1] : x[2]);
+      const float r0 = xi * 0.15915494309189535f;
+      for (int f = 0; f < F; ++f) {
+        const float r = __builtin_amdgcn_fractf(r0 * (float)(1 << f));
+        const float sn = __builtin_amdgcn_sinf(r), cs = __builtin_amdgcn_cosf(r);
+        const int j = q * F + f;
+        act[lds_idx<T>(m, col0 + j)] = to_t<T>(sn);
+        act[lds_idx<T>(m, col0 + 3 * F + j)] = to_t<T>(cs);
+        if (sv) {
+          sv[(int64_t)j * ld] = to_t<T>(sn);
+          sv[(int64_t)(3 * F + j) * ld] = to_t<T>(cs);
+        }
+      }
+    } else {
+      for (int k = 6 * F; k < width; ++k) {
+        const int a = k - 6 * F;
+        float v = a == 0 ? x[0] : 0.0f;
+        v = a == 1 ? x[1] : v;
+        v = a == 2 ? x[2] : v;
+        v = append ? v : 0.0f;
+        act[lds_idx<T>(m, col0 + k)] = to_t<T>(v);
+        if (sv) sv[(int64_t)k * ld] = to_t<T>(v);
+      }
+    }
+    return;
+  }
   for (int j = q; j < 3 * F; j += 4) {
     const int i = j / F, f = j - i * F;
     float xi = x[0];
     xi = i == 1 ? x[1] : xi;
     xi = i == 2 ? x[2] : xi;
     float sn, cs;
-    if constexpr (sizeof(T) == 4) {
-      sincosf(xi * (float)(1 << f), &sn, &cs);  // the parity mode keeps libm-accurate sin/cos
-    } else {
-      // bf16 mode: reduce to revolutions and use the hardware sin/cos (|error| ~1e-4 rad at the largest
-      // frequency, far below the 2^-9 relative rounding of the bf16 value it feeds)
-      float r = xi * (float)(1 << f) * 0.15915494309189535f;
-      r -= rintf(r);
-      sn = __builtin_amdgcn_sinf(r);
-      cs = __builtin_amdgcn_cosf(r);
-    }
+    sincosf(xi * (float)(1 << f), &sn, &cs);  // the parity mode keeps libm-accurate sin/cos
     act[lds_idx<T>(m, col0 + j)] = to_t<T>(sn);
     act[lds_idx<T>(m, col0 + 3 * F + j)] = to_t<T>(cs);
     if (sv) {
@@ -613,7 +638,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     gemm_lds<T, NT, MT>(Wt + lay.w_off[l], lay.kpad[l], nrow0, act, kc0, nkb, acc, lane, Wf + lay.b_off[l], &ring);
     if (l + 1 < lay.L) ring_fill<T, NT>(ring, Wt + lay.w_off[l + 1], lay.kpad[l + 1], nrow0, lay.kpad[l + 1] / KB, lane);
     else ring_fill<T, NT>(ring, Wt + lay.wint_off, 256, nrow0, 256 / KB, lane);
-    __syncthreads();
+    if (!(YANERF_ABLATE & 32)) __syncthreads();
     uint64_t bits = 0;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -622,7 +647,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
       for (int mt = 0; mt < MT; ++mt) {
         const Pk<T> h = pk_relu<T>(pk_make<T>(acc[nt][mt]));
         const int m = 16 * mt + li;
-        pk_lds<T>(act, m, n, h);
+        if (!(YANERF_ABLATE & 16)) pk_lds<T>(act, m, n, h);
+        else if (__float_as_uint(acc[nt][mt].x) == 0x7fc00001u) act[m] = (T)0;  // keep acc live
         if (saved && !(YANERF_ABLATE & 4)) {
           pk_store_rows<T>(saved + (SR.h0 + 256LL * l + n) * ld + p0 + m, ld, h);
           bits |= (uint64_t)pk_bits<T>(h) << ((nt * MT + mt) * 4);
@@ -630,29 +656,16 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
       }
     }
     if (saved && !(YANERF_ABLATE & 4)) masks[(((int64_t)l * gridDim.x + blockIdx.x) * WAVES + wave) * 64 + lane] = bits;
-    __syncthreads();
+    if (!(YANERF_ABLATE & 32)) __syncthreads();
   }
-  // ---- density head (VALU): sigma = w_d . h + b_d  (nerf_mlp.py:173; density_layer 256->1)
-  float sig;
-  {
-    const float* wd = Wf + lay.wd_off + 64 * q;
-    float s = 0.0f;
-#pragma unroll 2
-    for (int c = 0; c < ((YANERF_ABLATE & 8) ? 0 : 64 / EPC); ++c) {
-      float v[EPC];
-      unpack_chunk<T>(lds_chunk<T>(act, mt_, (64 * q) / EPC + c), v);
-#pragma unroll
-      for (int e = 0; e < EPC; e += 4) {
-        const f4 w = *(const f4*)(wd + c * EPC + e);
-        s += w.x * v[e];
-        s += w.y * v[e + 1];
-        s += w.z * v[e + 2];
-        s += w.w * v[e + 3];
-      }
-    }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    sig = s + Wf[lay.bd_off];
+  // ---- density head: sigma = w_d . h + b_d (nerf_mlp.py:173; density_layer 256->1) as one 16-row MFMA tile per
+  // wave over its 16 points (rows past 0 are zero weights); lanes g == 0 hold sigma of point 16 * wave + li.
+  // Shifting the LDS base by 16 * wave rows keeps the row swizzle (it depends on the row mod 16).
+  float sig = 0.f;
+  if (!(YANERF_ABLATE & 8)) {
+    f4 hacc[1][1];
+    gemm_lds<T, 1, 1>(Wt + lay.wdh_off, 256, 0, act + 16 * wave * ROW, 0, 256 / KB, hacc, lane);
+    sig = hacc[0][0].x + Wf[lay.bd_off];
   }
   // ---- intermediate_linear (no activation)
   gemm_lds<T, NT, MT>(Wt + lay.wint_off, 256, nrow0, act, 0, 256 / KB, acc, lane, Wf + lay.bint_off, &ring);
@@ -707,37 +720,21 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     }
   }
   __syncthreads();
-  // ---- output layer 128 -> color_dim + sigmoid (VALU)
+  // ---- output layer 128 -> color_dim + sigmoid, as for the density head (nerf_mlp.py:169-171)
   {
-    const float* wo = Wf + lay.wo_off;
-    float u[CMAX] = {0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; c < ((YANERF_ABLATE & 8) ? 0 : 32 / EPC); ++c) {
-      float v[EPC];
-      unpack_chunk<T>(lds_chunk<T>(act, mt_, (32 * q) / EPC + c), v);
+    f4 hacc[1][1] = {{f4{0.f, 0.f, 0.f, 0.f}}};
+    if (!(YANERF_ABLATE & 8))
+      gemm_lds<T, 1, 1>(Wt + lay.woh_off, HC, 0, act + 16 * wave * ROW, 0, HC / KB, hacc, lane);
+    const int64_t pw = p0 + 16 * wave + li;
+    if (g == 0 && pw < N) {
+      sigma[pw] = sig;
+      const float u[CMAX] = {hacc[0][0].x, hacc[0][0].y, hacc[0][0].z, hacc[0][0].w};
 #pragma unroll
       for (int j = 0; j < CMAX; ++j) {
         if (j < lay.cdim) {
-#pragma unroll
-          for (int e = 0; e < EPC; e += 4) {
-            const f4 w = *(const f4*)(wo + j * HC + 32 * q + c * EPC + e);
-            u[j] += w.x * v[e];
-            u[j] += w.y * v[e + 1];
-            u[j] += w.z * v[e + 2];
-            u[j] += w.w * v[e + 3];
-          }
+          float z = u[j] + Wf[lay.bo_off + j];
+          rgb[pw * lay.cdim + j] = 1.0f / (1.0f + expf(-z));
         }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < CMAX; ++j) {
-      u[j] += __shfl_xor(u[j], 1, 64);
-      u[j] += __shfl_xor(u[j], 2, 64);
-    }
-    if (q == 0 && p < N) {
-      sigma[p] = sig;
-      for (int j = 0; j < lay.cdim; ++j) {
-        float z = u[j] + Wf[lay.bo_off + j];
-        rgb[p * lay.cdim + j] = 1.0f / (1.0f + expf(-z));
       }
     }
   }
@@ -1074,11 +1071,13 @@ static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, const f
   add(h[0], L.hid, L.hid, L.wintT_off, 256, 256, L.hid, 0, 0, 1, 0);
   add(h[1], 1, L.hid, L.bint_off, 1, 256, L.hid, 0, 0, 0, 1);
   add(h[2], 1, L.hid, L.wd_off, 1, 256, L.hid, 0, 0, 0, 1);
+  add(h[2], 1, L.hid, L.wdh_off, 16, 256, L.hid, 0, 0, 0, 0);
   add(h[3], 1, 1, L.bd_off, 1, 4, 1, 0, 0, 0, 1);
   add(h[4], L.hdir, L.hid + L.dir_dim, L.wc_off, HC, KC, L.hid, 256, L.dir_dim, 0, 0);
   add(h[4], L.hdir, L.hid + L.dir_dim, L.wcT_off, 256, HC, L.hid, 0, 0, 1, 0);
   add(h[5], 1, L.hdir, L.bc_off, 1, HC, L.hdir, 0, 0, 0, 1);
   add(h[6], L.cdim, L.hdir, L.wo_off, CMAX, HC, L.hdir, 0, 0, 0, 1);
+  add(h[6], L.cdim, L.hdir, L.woh_off, 16, HC, L.hdir, 0, 0, 0, 0);
   add(h[7], 1, L.cdim, L.bo_off, 1, CMAX, L.cdim, 0, 0, 0, 1);
   return 0;
 }

@@ -864,6 +864,8 @@ struct DwJob {
   int x1_rows;
   int ktot;  // x0 + x1 ; slab row length = ktot + 1 (bias column)
   int bn;    // 256 | 128 | 64 rows per tile
+  int k_full;   // tiles of dw_bkmax(prec) columns, then (if k_tiles > k_full) one tail tile of bk_tail columns
+  int bk_tail;  // 64 | 128 | 256
   int k_tiles, tile_base;
   int64_t slab_off;
   float* W;  // grad of weight [a_rows][ktot] (reference layout)
@@ -876,7 +878,10 @@ struct DwJobs {
   int total_tiles;
   int64_t slab_elems;
 };
-constexpr int DW_BK = 128, DW_THREADS = 512;
+constexpr int DW_THREADS = 512;
+// widest dW column tile: bf16 is HBM/L2-bound (a 256-wide tile reads each dZ row once), fp32 is MFMA-bound and
+// runs faster with 128-wide tiles (measured: fp32 dW 8.3 ms vs 11.0 ms at 256; bf16 1.66 vs 2.0 ms at 128)
+__host__ __device__ constexpr int dw_bkmax(int prec) { return prec == YANERF_PREC_F32 ? 128 : 256; }
 
 template <typename T> __device__ __forceinline__ float hsum16(f4 v);
 template <> __device__ __forceinline__ float hsum16<float>(f4 v) { return (v.x + v.y) + (v.z + v.w); }
@@ -891,34 +896,36 @@ template <> __device__ __forceinline__ float hsum16<bf16_t>(f4 v) {
   return s;
 }
 
-// Stage ring: DW_STAGES buffers of up to (256 + DW_BK) rows x 128 B, filled by LDS-DMA (global_load_lds_dwordx4,
-// one wave-instruction = 8 whole rows) two stages ahead of the one being multiplied. The DMA destination is
-// lane-linear, so the XOR swizzle goes on the SOURCE chunk. One raw barrier per stage: after it every wave's DMA
-// for this stage has landed (each wave waited for its own with a counted vmcnt) and every wave is done reading
-// the buffer the next DMA overwrites.
-constexpr int DW_STAGES = 3, DW_STAGE_BYTES = (256 + DW_BK) * 128;
+// Stage ring: DW_STAGES buffers of up to 512 rows x 64 B (one K-block of points per row), filled by LDS-DMA
+// (global_load_lds_dwordx4; one wave-instruction = 16 whole rows) DW_STAGES-1 stages ahead of the one being
+// multiplied. The DMA destination is lane-linear, so the bank swizzle (16-byte chunk c of row r stored at
+// c ^ (2 * ((r >> 3) & 1)), conflict-free for the 16x16 fragment reads) goes on the SOURCE chunk. One raw barrier
+// per stage: after it every wave's DMA for this stage has landed (each wave waited for its own with a counted
+// vmcnt) and every wave is done reading the buffer the next DMA overwrites.
+constexpr int DW_STAGES = 4, DW_STAGE_BYTES = 512 * 64;
+__device__ __forceinline__ int dw_swz(int row, int c) { return c ^ (((row >> 3) & 1) << 1); }
 
-template <typename T, int BN>
-__device__ __forceinline__ void dw_tile(const DwJob& J, int kt, int s, int S, int64_t Npad, float* __restrict__ slab,
+template <typename T, int BN, int BK>
+__device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, int64_t Npad, float* __restrict__ slab,
                                         int64_t slab_elems, char* smem) {
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
-  constexpr int WN = BN / 64, WK = 8 / WN, WKW = DW_BK / WK, KTW = WKW / 16;
-  constexpr int ROWS = BN + DW_BK, PW = ROWS / 64;  // DMA wave-instructions per wave per stage
-  static_assert(ROWS % 64 == 0, "staging split");
+  constexpr int WN = BN / 64, WK0 = 8 / WN, WK = (BK / 16 < WK0) ? BK / 16 : WK0, KTW = BK / WK / 16;
+  static_assert(KTW >= 1 && WN * WK <= 8, "dW wave tiling");
+  constexpr int ROWS = BN + BK, PW = (ROWS + 127) / 128;  // DMA wave-instructions per wave per stage
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int wn = wave / WK, wk = wave % WK;
-  const int k0 = kt * DW_BK;
-  constexpr int SPTS = 2 * KB;  // points per stage (128 B per row)
-  const int64_t nst = Npad / SPTS, ld = row_ld(Npad, sizeof(T));
+  const bool mma_wave = wave < WN * WK;
+  const int64_t nst = Npad / KB, ld = row_ld(Npad, sizeof(T));
   const int64_t st_lo = nst * s / S, st_hi = nst * (s + 1) / S;
-  // this lane's DMA source rows: wave-instruction i covers rows 8 * (wave * PW + i) .. + 8, lane -> (row, slot)
+  // this lane's DMA source rows: wave-instruction i covers rows 16 * (8 i + wave) .. + 16, lane -> (row, slot);
+  // rows past ROWS (padding of the last instruction) re-read a valid row into unused LDS
   const T* src[PW];
 #pragma unroll
   for (int i = 0; i < PW; ++i) {
-    const int row = 8 * (wave * PW + i) + (lane >> 3);
-    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    const int row = 16 * (8 * i + wave) + (lane >> 2);
+    const int ch = dw_swz(row, lane & 3);
     const T* p;
     if (row < BN) {
       p = (const T*)J.A + (int64_t)(row < J.a_rows ? row : 0) * ld;  // rows past a_rows: any valid row (unused)
@@ -926,84 +933,105 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int kt, int s, int S, in
       const int k = k0 + row - BN;
       if (k < J.x0_rows) p = (const T*)J.X0 + (int64_t)k * ld;
       else if (k < J.ktot) p = (const T*)J.X1 + (int64_t)(k - J.x0_rows) * ld;
-      else p = (const T*)J.X0;  // columns past ktot are never stored
+      else p = (const T*)J.X0;  // columns past ktot / padding rows are never stored
     }
     src[i] = p + ch * EPC;
   }
   auto issue = [&](int64_t st) {
-    char* dst = smem + (int)(st % DW_STAGES) * DW_STAGE_BYTES + wave * PW * 1024;
+    char* dst = smem + (int)(st % DW_STAGES) * DW_STAGE_BYTES;
 #pragma unroll
     for (int i = 0; i < PW; ++i)
-      __builtin_amdgcn_global_load_lds(src[i] + st * SPTS, (__attribute__((address_space(3))) void*)(dst + i * 1024),
+      __builtin_amdgcn_global_load_lds(src[i] + st * KB, (__attribute__((address_space(3))) void*)(dst + (8 * i + wave) * 1024),
                                        16, 0, 0);
   };
   const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
-  constexpr int BPT = BN * 8 / DW_THREADS > 0 ? BN * 8 / DW_THREADS : 1;  // bias chunks per thread
+  constexpr int BPT = BN * 4 / DW_THREADS > 0 ? BN * 4 / DW_THREADS : 1;  // bias chunks per thread
   float rsum[BPT];
 #pragma unroll
   for (int i = 0; i < BPT; ++i) rsum[i] = 0.f;
-  const bool do_bias = (kt == 0);
+  const bool do_bias = (k0 == 0);
   f4 acc[4][KTW];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
     for (int q = 0; q < KTW; ++q) acc[nt][q] = zero;
-  if (st_lo < st_hi) issue(st_lo);
-  if (st_lo + 1 < st_hi) issue(st_lo + 1);
+#pragma unroll
+  for (int i = 0; i < DW_STAGES - 1; ++i)
+    if (st_lo + i < st_hi) issue(st_lo + i);
   for (int64_t st = st_lo; st < st_hi; ++st) {
-    // my DMA for stage st is complete once at most the next stage's PW remain outstanding
-    if (st + 1 < st_hi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+    // my DMA for stage st is complete once at most the later issued stages remain outstanding
+    const int64_t ahead = st_hi - 1 - st;  // stages issued after st (at most DW_STAGES - 2 here)
+    if (ahead >= DW_STAGES - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (DW_STAGES - 2)) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (st + 2 < st_hi) issue(st + 2);
+    if (st + DW_STAGES - 1 < st_hi) issue(st + DW_STAGES - 1);
     const char* buf = smem + (int)(st % DW_STAGES) * DW_STAGE_BYTES;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const int c = kb * 4 + g;
-      f4 a[4], b[KTW];
+    if (mma_wave) {
+      f4 a[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
         const int row = wn * 64 + 16 * nt + li;
-        a[nt] = *(const f4*)(buf + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+        a[nt] = *(const f4*)(buf + row * 64 + (dw_swz(row, g) << 4));
       }
+      // columns in groups of (at most) 4 tiles to bound the live fragment registers
+      constexpr int QG = KTW < 4 ? KTW : 4;
 #pragma unroll
-      for (int q = 0; q < KTW; ++q) {
-        const int row = BN + wk * WKW + 16 * q + li;
-        b[q] = *(const f4*)(buf + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+      for (int q0 = 0; q0 < KTW; q0 += QG) {
+        f4 b[QG];
+#pragma unroll
+        for (int q = 0; q < QG; ++q) {
+          const int row = BN + (wk * KTW + q0 + q) * 16 + li;
+          b[q] = *(const f4*)(buf + row * 64 + (dw_swz(row, g) << 4));
+        }
+        if constexpr (sizeof(T) == 4) {
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+              for (int q = 0; q < QG; ++q)
+                acc[nt][q0 + q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[nt][ks], b[q][ks], acc[nt][q0 + q], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int q = 0; q < QG; ++q) acc[nt][q0 + q] = mma_blk<T>(a[nt], b[q], acc[nt][q0 + q]);
+        }
       }
-      mma_grid<T, 4, KTW>(a, b, acc);
     }
     if (do_bias) {
 #pragma unroll
       for (int i = 0; i < BPT; ++i) {
-        const int idx = tid + DW_THREADS * i, row = idx >> 3, ch = idx & 7;
-        if (row < BN) rsum[i] += hsum16<T>(*(const f4*)(buf + row * 128 + (ch << 4)));
+        const int idx = tid + DW_THREADS * i, row = idx >> 2, ch = idx & 3;
+        if (row < BN) rsum[i] += hsum16<T>(*(const f4*)(buf + row * 64 + (ch << 4)));
       }
     }
   }
   float* out = slab + (int64_t)s * slab_elems + J.slab_off;
   const int kv = J.ktot + 1;
+  if (mma_wave) {
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt)
+    for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-    for (int q = 0; q < KTW; ++q) {
-      const int k = k0 + wk * WKW + 16 * q + li;
+      for (int q = 0; q < KTW; ++q) {
+        const int k = k0 + (wk * KTW + q) * 16 + li;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = wn * 64 + 16 * nt + 4 * g + r;
-        if (n < J.a_rows && k < J.ktot) out[(int64_t)n * kv + k] = acc[nt][q][r];
+        for (int r = 0; r < 4; ++r) {
+          const int n = wn * 64 + 16 * nt + 4 * g + r;
+          if (n < J.a_rows && k < J.ktot) out[(int64_t)n * kv + k] = acc[nt][q][r];
+        }
       }
-    }
+  }
   if (do_bias) {
 #pragma unroll
     for (int i = 0; i < BPT; ++i) {
-      const int idx = tid + DW_THREADS * i, row = idx >> 3;
+      const int idx = tid + DW_THREADS * i, row = idx >> 2;
       float v = rsum[i];
       v += __shfl_xor(v, 1, 64);
       v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      if ((idx & 7) == 0 && row < BN && row < J.a_rows) out[(int64_t)row * kv + J.ktot] = v;
+      if ((idx & 3) == 0 && row < BN && row < J.a_rows) out[(int64_t)row * kv + J.ktot] = v;
     }
   }
 }
@@ -1018,9 +1046,22 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   const DwJob& J = jobs.j[ji];
   const int local = b - J.tile_base * S;
   const int s = local / J.k_tiles, kt = local % J.k_tiles;
-  if (J.bn == 256) dw_tile<T, 256>(J, kt, s, S, Npad, slab, jobs.slab_elems, smem);
-  else if (J.bn == 128) dw_tile<T, 128>(J, kt, s, S, Npad, slab, jobs.slab_elems, smem);
-  else dw_tile<T, 64>(J, kt, s, S, Npad, slab, jobs.slab_elems, smem);
+  constexpr int BKMAX = dw_bkmax(sizeof(T) == 4 ? YANERF_PREC_F32 : YANERF_PREC_BF16);
+  const int k0 = kt * BKMAX;
+  const int bk = kt < J.k_full ? BKMAX : J.bk_tail;
+  const int64_t se = jobs.slab_elems;
+  if (J.bn == 256) {
+    if (bk == 256) dw_tile<T, 256, 256>(J, k0, s, S, Npad, slab, se, smem);
+    else if (bk == 128) dw_tile<T, 256, 128>(J, k0, s, S, Npad, slab, se, smem);
+    else dw_tile<T, 256, 64>(J, k0, s, S, Npad, slab, se, smem);
+  } else if (J.bn == 128) {
+    if (bk == 256) dw_tile<T, 128, 256>(J, k0, s, S, Npad, slab, se, smem);
+    else if (bk == 128) dw_tile<T, 128, 128>(J, k0, s, S, Npad, slab, se, smem);
+    else dw_tile<T, 128, 64>(J, k0, s, S, Npad, slab, se, smem);
+  } else {
+    if (bk == 256) dw_tile<T, 64, 256>(J, k0, s, S, Npad, slab, se, smem);
+    else dw_tile<T, 64, 128>(J, k0, s, S, Npad, slab, se, smem);
+  }
 }
 
 __global__ void dw_reduce_kernel(DwJobs jobs, int S, const float* __restrict__ slab) {
@@ -1092,6 +1133,17 @@ static int dw_splits(int total_tiles, int64_t n_stages) {
 }
 
 static int dw_bn(int a_rows) { return a_rows > 128 ? 256 : (a_rows > 64 ? 128 : 64); }
+// column tiling of one dW job: full dw_bkmax tiles, then one tail tile rounded up to 64 / 128 / 256 (>= 128 when
+// BN = 64, whose 8 waves need 16 columns each)
+static void dw_ktiles(int ktot, int bn, int prec, int* k_full, int* bk_tail, int* k_tiles) {
+  const int bkmax = dw_bkmax(prec);
+  *k_full = ktot / bkmax;
+  const int rem = ktot - *k_full * bkmax;
+  int bt = rem <= 64 ? 64 : (rem <= 128 ? 128 : 256);
+  if (bn == 64 && bt < 128) bt = 128;
+  *bk_tail = bt;
+  *k_tiles = *k_full + (rem > 0 ? 1 : 0);
+}
 
 // enumerate the dW jobs (shared by the size query and the launch)
 template <typename F>
@@ -1128,7 +1180,7 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     j.X0 = srow(x0); j.x0_rows = x0_rows; j.X1 = srow(x1); j.x1_rows = x1_rows;
     j.ktot = x0_rows + x1_rows;
     j.bn = dw_bn(a_rows);
-    j.k_tiles = (j.ktot + DW_BK - 1) / DW_BK;
+    dw_ktiles(j.ktot, j.bn, prec, &j.k_full, &j.bk_tail, &j.k_tiles);
     j.tile_base = D.total_tiles;
     D.total_tiles += j.k_tiles;
     j.slab_off = D.slab_elems;
@@ -1138,13 +1190,15 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
   });
 }
 
-static int64_t dw_slab_elems_for(const MlpLayout& L, int* total_tiles) {
+static int64_t dw_slab_elems_for(const MlpLayout& L, int prec, int* total_tiles) {
   int64_t e = 0;
   int tiles = 0;
   for_each_dw_job(L, [&](int64_t, int a_rows, int64_t, int x0_rows, int64_t, int x1_rows, int) {
     const int ktot = x0_rows + x1_rows;
     e += (int64_t)a_rows * (ktot + 1);
-    tiles += (ktot + DW_BK - 1) / DW_BK;
+    int kf, bt, kt;
+    dw_ktiles(ktot, dw_bn(a_rows), prec, &kf, &bt, &kt);
+    tiles += kt;
   });
   if (total_tiles) *total_tiles = tiles;
   return e;
@@ -1181,7 +1235,7 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   YN_LAUNCH_CHECK("mlp_backward_dx");
   DwJobs D;
   build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D);
-  const int S = dw_splits(D.total_tiles, Npad / (2 * Cfg<T>::KB));
+  const int S = dw_splits(D.total_tiles, Npad / Cfg<T>::KB);
   hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)(D.total_tiles * S)), dim3(DW_THREADS), 0, st, D, Npad, S, slab);
   YN_LAUNCH_CHECK("mlp_backward_dw");
   hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((D.slab_elems + 255) / 256)), dim3(256), 0, st, D, S, slab);
@@ -1237,9 +1291,9 @@ int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, 
   const GradRows GR = grad_rows(d->n_layers);
   int64_t grad_bytes = GR.rows * row_ld(Npad, elem_size(precision)) * (int64_t)elem_size(precision);
   int tiles = 0;
-  int64_t se = dw_slab_elems_for(L, &tiles);
+  int64_t se = dw_slab_elems_for(L, precision, &tiles);
   const int64_t kb = precision == YANERF_PREC_F32 ? Cfg<float>::KB : Cfg<bf16_t>::KB;
-  int S = dw_splits(tiles, Npad / (2 * kb));
+  int S = dw_splits(tiles, Npad / kb);
   return grad_bytes + (int64_t)S * se * 4;
 }
 

@@ -480,17 +480,20 @@ template <> __device__ __forceinline__ void pk_lds<bf16_t>(bf16_t* act, int m, i
 }
 // store the packed tile into 4 consecutive feature-major rows (stride ld)
 template <typename T> __device__ __forceinline__ void pk_store_rows(T* dst, int64_t ld, Pk<T> p);
+// Plain stores: the scattered 2-/4-byte row segments rely on write-combining in L2 (measured: non-temporal
+// stores made the bf16 forward 2.6x slower).
+template <typename V> __device__ __forceinline__ void st_stream(V* p, V v) { *p = v; }
 template <> __device__ __forceinline__ void pk_store_rows<float>(float* dst, int64_t ld, Pk<float> p) {
-  dst[0] = p.v.x;
-  dst[ld] = p.v.y;
-  dst[2 * ld] = p.v.z;
-  dst[3 * ld] = p.v.w;
+  st_stream(dst, p.v.x);
+  st_stream(dst + ld, p.v.y);
+  st_stream(dst + 2 * ld, p.v.z);
+  st_stream(dst + 3 * ld, p.v.w);
 }
 template <> __device__ __forceinline__ void pk_store_rows<bf16_t>(bf16_t* dst, int64_t ld, Pk<bf16_t> p) {
-  dst[0] = (bf16_t)p.w0;
-  dst[ld] = (bf16_t)(p.w0 >> 16);
-  dst[2 * ld] = (bf16_t)p.w1;
-  dst[3 * ld] = (bf16_t)(p.w1 >> 16);
+  st_stream(dst, (bf16_t)p.w0);
+  st_stream(dst + ld, (bf16_t)(p.w0 >> 16));
+  st_stream(dst + 2 * ld, (bf16_t)p.w1);
+  st_stream(dst + 3 * ld, (bf16_t)(p.w1 >> 16));
 }
 // zero the elements of v whose bit (bits >> sh .. sh+3) is clear
 __device__ __forceinline__ f4 apply_mask4(f4 v, uint64_t bits, int sh) {
@@ -902,8 +905,16 @@ template <> __device__ __forceinline__ float hsum16<bf16_t>(f4 v) {
 // c ^ (2 * ((r >> 3) & 1)), conflict-free for the 16x16 fragment reads) goes on the SOURCE chunk. One raw barrier
 // per stage: after it every wave's DMA for this stage has landed (each wave waited for its own with a counted
 // vmcnt) and every wave is done reading the buffer the next DMA overwrites.
-constexpr int DW_STAGES = 4, DW_STAGE_BYTES = 512 * 64;
-__device__ __forceinline__ int dw_swz(int row, int c) { return c ^ (((row >> 3) & 1) << 1); }
+#ifndef YANERF_DW_CPR
+#define YANERF_DW_CPR 4
+#endif
+constexpr int DW_CPR = YANERF_DW_CPR;      // 16-byte chunks per staged row (4: one K-block, 8: two)
+constexpr int DW_RB = 16 * DW_CPR;          // staged row bytes
+constexpr int DW_RPI = 64 / DW_CPR;         // rows per DMA wave-instruction
+constexpr int DW_STAGES = DW_CPR == 4 ? 4 : 2, DW_STAGE_BYTES = 512 * DW_RB;
+__device__ __forceinline__ int dw_swz(int row, int c) {
+  return DW_CPR == 4 ? (c ^ (((row >> 3) & 1) << 1)) : (c ^ ((row >> 1) & 7));
+}
 
 template <typename T, int BN, int BK>
 __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, int64_t Npad, float* __restrict__ slab,
@@ -911,21 +922,22 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
   constexpr int WN = BN / 64, WK0 = 8 / WN, WK = (BK / 16 < WK0) ? BK / 16 : WK0, KTW = BK / WK / 16;
   static_assert(KTW >= 1 && WN * WK <= 8, "dW wave tiling");
-  constexpr int ROWS = BN + BK, PW = (ROWS + 127) / 128;  // DMA wave-instructions per wave per stage
+  constexpr int ROWS = BN + BK, PW = (ROWS + 8 * DW_RPI - 1) / (8 * DW_RPI);  // DMA wave-instrs per wave per stage
+  constexpr int KBS = DW_CPR / 4;                                             // K-blocks per stage
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int wn = wave / WK, wk = wave % WK;
   const bool mma_wave = wave < WN * WK;
-  const int64_t nst = Npad / KB, ld = row_ld(Npad, sizeof(T));
+  const int64_t nst = Npad / (KB * KBS), ld = row_ld(Npad, sizeof(T));
   const int64_t st_lo = nst * s / S, st_hi = nst * (s + 1) / S;
-  // this lane's DMA source rows: wave-instruction i covers rows 16 * (8 i + wave) .. + 16, lane -> (row, slot);
+  // this lane's DMA source rows: wave-instruction i covers rows DW_RPI * (8 i + wave) .. + DW_RPI, lane -> (row, slot);
   // rows past ROWS (padding of the last instruction) re-read a valid row into unused LDS
   const T* src[PW];
 #pragma unroll
   for (int i = 0; i < PW; ++i) {
-    const int row = 16 * (8 * i + wave) + (lane >> 2);
-    const int ch = dw_swz(row, lane & 3);
+    const int row = DW_RPI * (8 * i + wave) + lane / DW_CPR;
+    const int ch = dw_swz(row, lane % DW_CPR);
     const T* p;
     if (row < BN) {
       p = (const T*)J.A + (int64_t)(row < J.a_rows ? row : 0) * ld;  // rows past a_rows: any valid row (unused)
@@ -941,11 +953,11 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
     char* dst = smem + (int)(st % DW_STAGES) * DW_STAGE_BYTES;
 #pragma unroll
     for (int i = 0; i < PW; ++i)
-      __builtin_amdgcn_global_load_lds(src[i] + st * KB, (__attribute__((address_space(3))) void*)(dst + (8 * i + wave) * 1024),
-                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src[i] + st * (KB * KBS),
+                                       (__attribute__((address_space(3))) void*)(dst + (8 * i + wave) * 1024), 16, 0, 0);
   };
   const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
-  constexpr int BPT = BN * 4 / DW_THREADS > 0 ? BN * 4 / DW_THREADS : 1;  // bias chunks per thread
+  constexpr int BPT = BN * DW_CPR / DW_THREADS > 0 ? BN * DW_CPR / DW_THREADS : 1;  // bias chunks per thread
   float rsum[BPT];
 #pragma unroll
   for (int i = 0; i < BPT; ++i) rsum[i] = 0.f;
@@ -961,19 +973,23 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
   for (int64_t st = st_lo; st < st_hi; ++st) {
     // my DMA for stage st is complete once at most the later issued stages remain outstanding
     const int64_t ahead = st_hi - 1 - st;  // stages issued after st (at most DW_STAGES - 2 here)
+    static_assert(DW_STAGES >= 2 && DW_STAGES <= 5, "wait ladder below");
     if (ahead >= DW_STAGES - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (DW_STAGES - 2)) : "memory");
+    else if (DW_STAGES == 5 && ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * 2) : "memory");
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (st + DW_STAGES - 1 < st_hi) issue(st + DW_STAGES - 1);
     const char* buf = smem + (int)(st % DW_STAGES) * DW_STAGE_BYTES;
+#pragma unroll
+    for (int kb = 0; kb < KBS; ++kb)
     if (mma_wave) {
       f4 a[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
         const int row = wn * 64 + 16 * nt + li;
-        a[nt] = *(const f4*)(buf + row * 64 + (dw_swz(row, g) << 4));
+        a[nt] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, kb * 4 + g) << 4));
       }
       // columns in groups of (at most) 4 tiles to bound the live fragment registers
       constexpr int QG = KTW < 4 ? KTW : 4;
@@ -983,7 +999,7 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
 #pragma unroll
         for (int q = 0; q < QG; ++q) {
           const int row = BN + (wk * KTW + q0 + q) * 16 + li;
-          b[q] = *(const f4*)(buf + row * 64 + (dw_swz(row, g) << 4));
+          b[q] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, kb * 4 + g) << 4));
         }
         if constexpr (sizeof(T) == 4) {
 #pragma unroll
@@ -1004,8 +1020,8 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
     if (do_bias) {
 #pragma unroll
       for (int i = 0; i < BPT; ++i) {
-        const int idx = tid + DW_THREADS * i, row = idx >> 2, ch = idx & 3;
-        if (row < BN) rsum[i] += hsum16<T>(*(const f4*)(buf + row * 64 + (ch << 4)));
+        const int idx = tid + DW_THREADS * i, row = idx / DW_CPR, ch = idx % DW_CPR;
+        if (row < BN) rsum[i] += hsum16<T>(*(const f4*)(buf + row * DW_RB + (ch << 4)));
       }
     }
   }
@@ -1027,11 +1043,11 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
   if (do_bias) {
 #pragma unroll
     for (int i = 0; i < BPT; ++i) {
-      const int idx = tid + DW_THREADS * i, row = idx >> 2;
+      const int idx = tid + DW_THREADS * i, row = idx / DW_CPR;
       float v = rsum[i];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      if ((idx & 3) == 0 && row < BN && row < J.a_rows) out[(int64_t)row * kv + J.ktot] = v;
+#pragma unroll
+      for (int o = 1; o < DW_CPR; o <<= 1) v += __shfl_xor(v, o, 64);
+      if (idx % DW_CPR == 0 && row < BN && row < J.a_rows) out[(int64_t)row * kv + J.ktot] = v;
     }
   }
 }
@@ -1235,7 +1251,7 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   YN_LAUNCH_CHECK("mlp_backward_dx");
   DwJobs D;
   build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D);
-  const int S = dw_splits(D.total_tiles, Npad / Cfg<T>::KB);
+  const int S = dw_splits(D.total_tiles, Npad / (Cfg<T>::KB * (DW_CPR / 4)));
   hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)(D.total_tiles * S)), dim3(DW_THREADS), 0, st, D, Npad, S, slab);
   YN_LAUNCH_CHECK("mlp_backward_dw");
   hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((D.slab_elems + 255) / 256)), dim3(256), 0, st, D, S, slab);
@@ -1293,7 +1309,7 @@ int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, 
   int tiles = 0;
   int64_t se = dw_slab_elems_for(L, precision, &tiles);
   const int64_t kb = precision == YANERF_PREC_F32 ? Cfg<float>::KB : Cfg<bf16_t>::KB;
-  int S = dw_splits(tiles, Npad / kb);
+  int S = dw_splits(tiles, Npad / (kb * (DW_CPR / 4)));
   return grad_bytes + (int64_t)S * se * 4;
 }
 

@@ -2,7 +2,7 @@
 """Benchmark: NeRF training-step throughput (rays/s) on Lego 800x800, 64 coarse + 128 fine samples
 (BASELINE.json configs[1]; configs[2] at N GPUs), MI355X HIP path.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32|bf16] [--rays 4096]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp32|bf16|fp32x3] [--rays 4096]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
 
@@ -40,7 +40,9 @@ from yanerf_amd.utils.config import Config  # noqa: E402
 METRIC = "rays/sec (train step) + PSNR, Lego 800×800 64c+128f, 1/2/4/8 MI355X"
 MAC_PER_POINT = 589_952  # 63*256 + 4*256^2 + 319*256 + 2*256^2 + 256^2 + 256 + 256*128 + 128*3
 MAC_PER_RAY_PASS = 27 * 128  # LinearWithRepeat direction term, once per ray per pass
-PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}  # MI355X dense matrix peaks (MI355X_MICROARCH.md)
+# MI355X dense matrix peaks (MI355X_MICROARCH.md); fp32x3 runs six bf16 MFMAs per fp32 product, so its ceiling
+# for fp32 work is the bf16 peak / 6
+PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "fp32x3": 2500.0 / 6}
 
 
 def synthetic_pose(theta, phi, radius=4.0):
@@ -153,7 +155,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--precision", default=os.environ.get("YANERF_BENCH_PRECISION", "fp32"), choices=["fp32", "bf16"])
+    ap.add_argument("--precision", default=os.environ.get("YANERF_BENCH_PRECISION", "fp32"), choices=list(PEAK_TFLOPS))
     ap.add_argument("--rays", type=int, default=None, help="rays per rank per step (default: config, 4096)")
     ap.add_argument("--config", default=str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -225,7 +227,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32" if args.precision == "fp32" else "bf16",
+        "dtype": {"fp32": "f32", "bf16": "bf16", "fp32x3": "f32 (3xbf16 split MFMA)"}[args.precision],
         "data": "synthetic (random 800x800 target per rank, 40 spherical poses; random-init Lego MLPs)",
         "config": {"workload": "lego_800x800_64c_128f_train_step", "rays_per_gpu": R, "pts_per_ray": Pc + Pf,
                    "global_batch_rays": R * world, "parallelism": f"dp{world}", "precision": args.precision},

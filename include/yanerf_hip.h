@@ -30,6 +30,10 @@ extern "C" {
 
 #define YANERF_PREC_F32 0  /* exact fp32: f32-input MFMA (v_mfma_f32_16x16x4_f32), fp32 activations */
 #define YANERF_PREC_BF16 1 /* bf16 MFMA (v_mfma_f32_16x16x32_bf16), fp32 accumulate, bf16 activations */
+/* fp32 split into three bf16 terms (x = x0 + x1 + x2 exactly): six bf16 MFMAs per product (all terms down to
+   2^-24 relative), fp32 accumulate, fp32 saved activations / gradients. fp32-class accuracy at ~2.6x the fp32
+   MFMA rate. */
+#define YANERF_PREC_F32X3 2
 
 const char* yanerf_last_error(void);
 int yanerf_version(void);

@@ -100,11 +100,16 @@ def test_raysampler(pkg, golden, tag, cfg):
 
 
 # ------------------------------------------------------------------------------------------- MLP
+# the fp32-class modes: exact fp32 MFMA, and fp32 as three bf16 terms (six bf16 MFMAs per product) -- same gates
+FP32_MODES = ["fp32", "fp32x3"]
+
+
+@pytest.mark.parametrize("precision", FP32_MODES)
 @pytest.mark.parametrize("tag", ["small", "lego"])
-def test_mlp_fwd_bwd_fp32(pkg, golden, tag):
+def test_mlp_fwd_bwd_fp32(pkg, golden, tag, precision):
     g = golden(f"mlp_{tag}")
     arch = SMALL_ARCH if tag == "small" else LEGO_ARCH
-    m, params = build_mlp(pkg, arch, int(g["seed"]))
+    m, params = build_mlp(pkg, arch, int(g["seed"]), precision=precision)
     o, d, z = t(g["origins"]), t(g["directions"]), t(g["lengths"])
     out = m(o, d, z)
     sig, rgb = out["rays_densities"], out["rays_features"]
@@ -140,14 +145,15 @@ def test_mlp_bf16_bounds(pkg, golden):
             close(np.linalg.norm(n(p.grad).astype(np.float64)), nn, 0.1 * nn)
 
 
-def test_mlp_large_vs_oracle(pkg):
+@pytest.mark.parametrize("precision", FP32_MODES)
+def test_mlp_large_vs_oracle(pkg, precision):
     """65,536 points (1024 rays x 64) of the Lego MLP against the oracle on a 2,048-point subset."""
     rng = np.random.default_rng(0)
     R, P = 1024, 64
     o = (rng.standard_normal((R, 3)) * 0.3 + [0, 0, 4]).astype(np.float32)
     d = rng.standard_normal((R, 3)).astype(np.float32)
     z = np.sort(rng.uniform(2, 6, (R, P)).astype(np.float32), -1)
-    m, params = build_mlp(pkg, LEGO_ARCH, 31)
+    m, params = build_mlp(pkg, LEGO_ARCH, 31, precision=precision)
     out = m(t(o), t(d), t(z))
     sub = slice(0, 32)
     sig_o, rgb_o, _ = O.nerf_mlp_forward(params, O.MLPArch.from_dict(LEGO_ARCH), o[sub], d[sub], z[sub])
@@ -256,9 +262,10 @@ def _lego_pipeline(pkg, seeds, n_rays=4096, noise=0.2, precision="fp32"):
     return pipe
 
 
-def test_render_eval_lego(pkg, golden):
+@pytest.mark.parametrize("precision", FP32_MODES)
+def test_render_eval_lego(pkg, golden, precision):
     g = golden("render_eval_lego")
-    pipe = _lego_pipeline(pkg, g["seeds"])
+    pipe = _lego_pipeline(pkg, g["seeds"], precision=precision)
     pipe.eval()
     H, W = int(g["H"]), int(g["W"])
     R = H * W
@@ -288,10 +295,11 @@ def test_render_eval_lego(pkg, golden):
     close(n(preds["loss_rgb_mse"]), g["loss_rgb_mse"], 2e-6)
 
 
-def test_train_step_lego(pkg, golden):
+@pytest.mark.parametrize("precision", FP32_MODES)
+def test_train_step_lego(pkg, golden, precision):
     g = golden("train_step_lego")
     R = int(g["n_rays"])
-    pipe = _lego_pipeline(pkg, g["seeds"], n_rays=R)
+    pipe = _lego_pipeline(pkg, g["seeds"], n_rays=R, precision=precision)
     pipe.train()
     ops = pkg["ops"]
     img = torch.zeros(1, 800, 800, 3, device=DEV)

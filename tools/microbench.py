@@ -20,7 +20,7 @@ def main(R=4096, P=192, reps=10):
     dev = torch.device("cuda:0")
     L = _C.lib()
     res = {}
-    for prec in ("fp32", "bf16"):
+    for prec in (sys.argv[1].split(",") if len(sys.argv) > 1 else ("fp32", "bf16", "fp32x3")):
         torch.manual_seed(0)
         m = MODELS.build(dict(type="NeRFMLP", precision=prec)).to(dev)
         spec = m.spec()

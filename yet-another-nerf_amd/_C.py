@@ -14,6 +14,7 @@ LIB_PATH = Path(os.environ.get("YANERF_HIP_LIB", Path(__file__).resolve().parent
 
 PREC_F32 = 0
 PREC_BF16 = 1
+PREC_F32X3 = 2  # fp32 as three bf16 terms, six bf16 MFMAs per product (include/yanerf_hip.h)
 
 # every symbol include/yanerf_hip.h declares (checked by tests/test_capi.py)
 EXPORTS = (

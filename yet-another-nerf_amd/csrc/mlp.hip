@@ -36,11 +36,35 @@ namespace yanerf {
 
 typedef unsigned short bf16_t;
 
+// fp32 emulated on bf16 MFMAs: every operand is split into three bf16 planes (x = x0 + x1 + x2 exactly) and a
+// product is the six terms x_i y_j with i + j <= 2 (the dropped ones are below 2^-24 relative)
+struct x3_t {};
+
+// per precision: point tile M, waves per workgroup, elements per 16-byte chunk (EPC) and per 64-byte K-block (KB),
+// weight-ring depth, occupancy target (waves per SIMD), operand planes, and the element types of the LDS tile,
+// of the saved activations / gradients in HBM and of the packed weights
 template <typename T> struct Cfg;
-template <> struct Cfg<float> { static constexpr int M = 64, WAVES = 4, EPC = 4, KB = 16, APREF = 1, LOWREG = 0, WPE = 2; };
+template <> struct Cfg<float> {
+  static constexpr int M = 64, WAVES = 4, EPC = 4, KB = 16, APREF = 1, LOWREG = 0, WPE = 2, PLANES = 1;
+  typedef float lds_t;
+  typedef float st_t;
+  typedef float w_t;
+};
 template <> struct Cfg<bf16_t> {
   static constexpr int M = 128, WAVES = 8, EPC = 8, KB = 32, APREF = 3, LOWREG = YANERF_LOWREG, WPE = LOWREG ? 4 : 2;
+  static constexpr int PLANES = 1;
+  typedef bf16_t lds_t;
+  typedef bf16_t st_t;
+  typedef bf16_t w_t;
 };
+template <> struct Cfg<x3_t> {
+  static constexpr int M = 64, WAVES = 8, EPC = 8, KB = 32, APREF = 2, LOWREG = 0, WPE = 2, PLANES = 3;
+  typedef bf16_t lds_t;
+  typedef float st_t;
+  typedef bf16_t w_t;
+};
+template <typename T> constexpr bool is_x3 = false;
+template <> constexpr bool is_x3<x3_t> = true;
 
 constexpr int ROW = 320;    // LDS row length (elements)
 constexpr int PE_COL = 256; // xyz-PE / dir-PE column base
@@ -61,6 +85,7 @@ struct MlpLayout {
   int64_t wint_off, wintT_off, wc_off, wcT_off;
   int64_t wdh_off, woh_off;  // density / colour-output heads as 16-row GEMM operands (rows past 1 / cdim are 0)
   int64_t t_elems;
+  int64_t t_plane;  // elements between the bf16 planes of an x3 operand (0 otherwise)
   int64_t f_base;  // byte offset of the fp32 section
   int64_t b_off[MAXL];
   int64_t bint_off, bc_off, wd_off, bd_off, wo_off, bo_off;
@@ -98,12 +123,22 @@ __host__ __device__ inline GradRows grad_rows(int L) {
 
 // ReLU masks, kept for the dX kernel instead of re-reading the saved activations:
 //  * trunk layers: the forward and dX kernels share one wave->tile decomposition (Cfg<T>), so every lane packs
-//    ITS OWN 4 bits of each of its NT*MT = 16 accumulator tiles into one u64 per layer
-//    (index ((layer * n_wg + wg) * WAVES + wave) * 64 + lane): one coalesced 8-byte load per lane in dX;
+//    ITS OWN 4 bits of each of its NT*MT (16; 8 for x3) accumulator tiles into one u64 per layer
+//    (index ((layer * n_wg + wg) * WAVES + wave) * 64 + lane, trunk_mask_words per layer): one coalesced 8-byte
+//    load per lane in dX;
 //  * colour hidden layer: the __ballot of each 16x16 tile (4 u64 words; bit `lane` = feature 4*(lane>>4)+r of
 //    point lane&15), read per point by the VALU colour-head backward.
-// Both are 256 bits per point per layer.
+// Both are 256 bits per point per layer (trunk: 512 in x3, whose 8-wave tiles hold 64 points).
 __host__ __device__ inline int64_t mask_words_per_slot(int64_t Npad) { return Npad / 16 * 16 * 4; }
+// u64 words of one trunk layer's per-lane masks: one per lane of every wave of every point tile
+template <typename T> __host__ __device__ inline int64_t trunk_mask_words(int64_t Npad) {
+  return Npad / Cfg<T>::M * Cfg<T>::WAVES * 64;
+}
+static int64_t trunk_mask_words_prec(int prec, int64_t Npad) {
+  return prec == YANERF_PREC_F32    ? trunk_mask_words<float>(Npad)
+         : prec == YANERF_PREC_BF16 ? trunk_mask_words<bf16_t>(Npad)
+                                    : trunk_mask_words<x3_t>(Npad);
+}
 __device__ __forceinline__ int64_t mask_index(int64_t Npad, int slot, int64_t pt16, int ft) {
   return (((int64_t)slot * (Npad / 16) + pt16) * 16 + ft) * 4;
 }
@@ -119,9 +154,15 @@ static int64_t saved_t_bytes(int L, int64_t Npad, size_t es) {
   return saved_rows(L).rows * row_ld(Npad, es) * (int64_t)es;
 }
 
-static int64_t tile_m(int prec) { return prec == YANERF_PREC_F32 ? Cfg<float>::M : Cfg<bf16_t>::M; }
+static int64_t tile_m(int prec) {
+  return prec == YANERF_PREC_F32 ? Cfg<float>::M : prec == YANERF_PREC_BF16 ? Cfg<bf16_t>::M : Cfg<x3_t>::M;
+}
 static int64_t npad_of(int prec, int64_t n) { int64_t M = tile_m(prec); return (n + M - 1) / M * M; }
-static size_t elem_size(int prec) { return prec == YANERF_PREC_F32 ? 4 : 2; }
+// element size of the saved activations / gradient rows (fp32 for both fp32 modes)
+static size_t elem_size(int prec) { return prec == YANERF_PREC_BF16 ? 2 : 4; }
+// element size and plane count of the packed GEMM operands
+static size_t w_size(int prec) { return prec == YANERF_PREC_F32 ? 4 : 2; }
+static int w_planes(int prec) { return prec == YANERF_PREC_F32X3 ? 3 : 1; }
 
 static int check_desc(const yanerf_mlp_desc* d) {
   YN_CHECK(d, "mlp: null desc");
@@ -168,7 +209,8 @@ static MlpLayout make_layout(const yanerf_mlp_desc* d, int prec) {
   L.wdh_off = t; t += 16LL * 256;
   L.woh_off = t; t += 16LL * HC;
   L.t_elems = t;
-  int64_t tb = t * (int64_t)elem_size(prec);
+  L.t_plane = w_planes(prec) > 1 ? t : 0;
+  int64_t tb = t * (int64_t)w_size(prec) * w_planes(prec);
   L.f_base = (tb + 255) / 256 * 256;
   int64_t f = 0;
   for (int l = 0; l < L.L; ++l) { L.b_off[l] = f; f += 256; }
@@ -201,7 +243,8 @@ struct PackJobs {
 };
 
 template <typename T>
-__global__ void pack_kernel(PackJobs jobs, T* __restrict__ dst_t, float* __restrict__ dst_f) {
+__global__ void pack_kernel(PackJobs jobs, typename Cfg<T>::w_t* __restrict__ dst_t, float* __restrict__ dst_f,
+                            int64_t t_plane) {
   int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= jobs.total) return;
   int lo = 0, hi = jobs.n - 1;
@@ -227,8 +270,20 @@ __global__ void pack_kernel(PackJobs jobs, T* __restrict__ dst_t, float* __restr
     constexpr int KB = Cfg<T>::KB, EPC = Cfg<T>::EPC;
     const int64_t fi = (((int64_t)(r >> 4) * (J.cols / KB) + c / KB) * 64 + ((c % KB) / EPC) * 16 + (r & 15)) * EPC +
                        c % EPC;
-    if constexpr (sizeof(T) == 4) dst_t[J.dst_off + fi] = v;
-    else dst_t[J.dst_off + fi] = f2bf(v);
+    if constexpr (is_x3<T>) {
+      // three bf16 planes, x = x0 + x1 + x2 exactly (each residual is exact in fp32)
+      const bf16_t x0 = f2bf(v);
+      const float r1 = v - bf2f(x0);
+      const bf16_t x1 = f2bf(r1);
+      const bf16_t x2 = f2bf(r1 - bf2f(x1));
+      dst_t[J.dst_off + fi] = x0;
+      dst_t[t_plane + J.dst_off + fi] = x1;
+      dst_t[2 * t_plane + J.dst_off + fi] = x2;
+    } else if constexpr (sizeof(T) == 4) {
+      dst_t[J.dst_off + fi] = v;
+    } else {
+      dst_t[J.dst_off + fi] = f2bf(v);
+    }
   }
 }
 
@@ -236,13 +291,42 @@ __global__ void pack_kernel(PackJobs jobs, T* __restrict__ dst_t, float* __restr
 template <typename T> __device__ __forceinline__ int swz(int m, int c);
 template <> __device__ __forceinline__ int swz<float>(int m, int c) { return c ^ (m & 15); }
 template <> __device__ __forceinline__ int swz<bf16_t>(int m, int c) { return c ^ ((m >> 1) & 7); }
+template <> __device__ __forceinline__ int swz<x3_t>(int m, int c) { return c ^ ((m >> 1) & 7); }
 
 template <typename T> __device__ __forceinline__ int lds_idx(int m, int col) {
   constexpr int EPC = Cfg<T>::EPC;
   return m * ROW + swz<T>(m, col / EPC) * EPC + (col % EPC);
 }
-template <typename T> __device__ __forceinline__ f4 lds_chunk(const T* act, int m, int c) {
+template <typename T> __device__ __forceinline__ f4 lds_chunk(const typename Cfg<T>::lds_t* act, int m, int c) {
   return *(const f4*)(act + m * ROW + swz<T>(m, c) * Cfg<T>::EPC);
+}
+// x3: split an fp32 value into three bf16 terms, v = t0 + t1 + t2 exactly (each residual is exact in fp32)
+__device__ __forceinline__ void split3(float v, bf16_t& t0, bf16_t& t1, bf16_t& t2) {
+  t0 = f2bf(v);
+  const float r1 = v - bf2f(t0);
+  t1 = f2bf(r1);
+  t2 = f2bf(r1 - bf2f(t1));
+}
+// write one value into LDS element (m, col) in T's representation (x3: three planes, plane stride M * ROW)
+template <typename T> __device__ __forceinline__ void lds_put1(typename Cfg<T>::lds_t* act, int m, int col, float v) {
+  const int i = m * ROW + swz<T>(m, col / Cfg<T>::EPC) * Cfg<T>::EPC + (col % Cfg<T>::EPC);
+  if constexpr (is_x3<T>) {
+    constexpr int PL = Cfg<T>::M * ROW;
+    bf16_t t0, t1, t2;
+    split3(v, t0, t1, t2);
+    act[i] = t0;
+    act[PL + i] = t1;
+    act[2 * PL + i] = t2;
+  } else if constexpr (sizeof(typename Cfg<T>::lds_t) == 4) {
+    act[i] = v;
+  } else {
+    act[i] = f2bf(v);
+  }
+}
+// one value in T's saved / gradient row representation
+template <typename T> __device__ __forceinline__ typename Cfg<T>::st_t to_st(float v) {
+  if constexpr (sizeof(typename Cfg<T>::st_t) == 4) return v;
+  else return f2bf(v);
 }
 template <typename T> __device__ __forceinline__ T to_t(float v);
 template <> __device__ __forceinline__ float to_t<float>(float v) { return v; }
@@ -262,6 +346,8 @@ template <> __device__ __forceinline__ f4 mma_blk<float>(f4 a, f4 b, f4 c) {
 template <> __device__ __forceinline__ f4 mma_blk<bf16_t>(f4 a, f4 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a), __builtin_bit_cast(bf8, b), c, 0, 0, 0);
 }
+// (x3 operands are single bf16 planes at this level; gemm_lds combines the six plane products)
+template <> __device__ __forceinline__ f4 mma_blk<x3_t>(f4 a, f4 b, f4 c) { return mma_blk<bf16_t>(a, b, c); }
 
 // acc[i][j] += A_i x B_j over one 64-byte K-block for a grid of independent accumulators. fp32: the four
 // 16x16x4 k-steps are the OUTER loop so consecutive MFMAs never depend on each other (dependent-accumulator
@@ -302,18 +388,21 @@ __device__ __forceinline__ void mma_grid(const f4 (&a)[NI], const f4 (&b)[NJ], f
 // last K-block re-read the last block (uniform, in-bounds, a few redundant L2 hits per layer).
 // bf16 weight-fragment ring (see gemm_lds). A caller may fill it for the NEXT GEMM before running the current
 // layer's epilogue, so that GEMM starts on weights already in registers instead of an L2 round trip.
-template <typename T, int NT> struct ARing { f4 a[Cfg<T>::APREF][NT]; };
+template <typename T, int NT> struct ARing { f4 a[Cfg<T>::APREF][Cfg<T>::PLANES][NT]; };
 template <typename T, int NT>
-__device__ __forceinline__ void ring_fill(ARing<T, NT>& R, const T* __restrict__ W, int ldw, int nrow0, int nkb,
-                                          int lane) {
-  if constexpr (sizeof(T) == 2) {
-    constexpr int D = Cfg<T>::APREF, EPC = Cfg<T>::EPC, KB = Cfg<T>::KB, FRAG = 64 * EPC;
+__device__ __forceinline__ void ring_fill(ARing<T, NT>& R, const typename Cfg<T>::w_t* __restrict__ W, int64_t wplane,
+                                          int ldw, int nrow0, int nkb, int lane) {
+  if constexpr (sizeof(typename Cfg<T>::w_t) == 2) {
+    constexpr int D = Cfg<T>::APREF, EPC = Cfg<T>::EPC, KB = Cfg<T>::KB, FRAG = 64 * EPC, NP = Cfg<T>::PLANES;
 #pragma unroll
     for (int r = 0; r < D; ++r) {
       const int k = r < nkb ? r : nkb - 1;
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        R.a[r][nt] = *(const f4*)(W + ((size_t)((nrow0 >> 4) + nt) * (ldw / KB) * 64 + lane) * EPC + k * FRAG);
+      for (int pl = 0; pl < NP; ++pl)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          R.a[r][pl][nt] = *(const f4*)(W + pl * wplane +
+                                        ((size_t)((nrow0 >> 4) + nt) * (ldw / KB) * 64 + lane) * EPC + k * FRAG);
     }
   }
 }
@@ -321,9 +410,9 @@ __device__ __forceinline__ void ring_fill(ARing<T, NT>& R, const T* __restrict__
 // Accumulator layout: acc[nt][mt] lane (g, li) holds features nrow0 + 16nt + 4g .. +3 of point 16mt + li. The
 // accumulators start from the bias when one is given (the reference's addmm also accumulates onto the bias).
 template <typename T, int NT, int MT>
-__device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int nrow0, const T* act, int kc0, int nkb,
-                                         f4 (&acc)[NT][MT], int lane, const float* __restrict__ bias = nullptr,
-                                         ARing<T, NT>* pre = nullptr) {
+__device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict__ W, int64_t wplane, int ldw, int nrow0,
+                                         const typename Cfg<T>::lds_t* act, int kc0, int nkb, f4 (&acc)[NT][MT],
+                                         int lane, const float* __restrict__ bias, ARing<T, NT>& R) {
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
   const int g = lane >> 4, li = lane & 15;
 #pragma unroll
@@ -333,10 +422,58 @@ __device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int n
     for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = b0;
   }
   // W is in A-fragment order (pack_kernel): row tile rt, K-block kb at ((rt * ldw / KB + kb) * 64 + lane) * EPC
-  const T* wp[NT];
+  const typename Cfg<T>::w_t* wp[NT];
   constexpr int FRAG = 64 * EPC;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) wp[nt] = W + ((size_t)((nrow0 >> 4) + nt) * (ldw / KB) * 64 + lane) * EPC;
+  if constexpr (is_x3<T>) {
+    // x3: per K-block and (nt, mt) the six bf16 products w_i x a_j (i + j <= 2), smallest first, each term issued
+    // across all accumulators before the next so consecutive MFMAs never share one
+    constexpr int D = Cfg<T>::APREF, PL = Cfg<T>::M * ROW;
+    f4(&a)[D][3][NT] = R.a;
+    f4 b[3][MT];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) b[pl][mt] = lds_chunk<T>(act + pl * PL, 16 * mt + li, kc0 + g);
+    auto step = [&](int kb, f4(&ar)[3][NT], bool refill) {
+      const int kn = kb + 1 < nkb ? kb + 1 : kb;
+      f4 bn[3][MT];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) bn[pl][mt] = lds_chunk<T>(act + pl * PL, 16 * mt + li, kc0 + kn * 4 + g);
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int TI[6] = {2, 1, 0, 1, 0, 0}, TJ[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+      for (int t = 0; t < 6; ++t)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = mma_blk<bf16_t>(ar[TI[t]][nt], b[TJ[t]][mt], acc[nt][mt]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (refill) {
+        const int ka = kb + D < nkb ? kb + D : nkb - 1;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) ar[pl][nt] = *(const f4*)(wp[nt] + pl * wplane + ka * FRAG);
+      }
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) b[pl][mt] = bn[pl][mt];
+    };
+    int kb = 0;
+    for (; kb + D <= nkb; kb += D) {
+#pragma unroll
+      for (int r = 0; r < D; ++r) step(kb + r, a[r], true);
+    }
+#pragma unroll
+    for (int r = 0; r < D - 1; ++r)
+      if (kb + r < nkb) step(kb + r, a[r], false);
+    return;
+  }
   if constexpr (sizeof(T) == 2 && Cfg<T>::LOWREG) {
     // two workgroups per CU (<= 128 VGPRs): no LDS double buffer, a 2-deep weight ring; the other workgroup's
     // waves cover the LDS / L2 latency
@@ -372,9 +509,7 @@ __device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int n
   }
   if constexpr (sizeof(T) == 2) {
     constexpr int D = Cfg<T>::APREF;
-    ARing<T, NT> own;
-    if (!pre) ring_fill<T, NT>(own, W, ldw, nrow0, nkb, lane);
-    f4(&a)[D][NT] = pre ? pre->a : own.a;
+    f4(&a)[D][1][NT] = R.a;
     f4 b[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) b[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + g);
@@ -398,12 +533,12 @@ __device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int n
     int kb = 0;
     for (; kb + D <= nkb; kb += D) {
 #pragma unroll
-      for (int r = 0; r < D; ++r) step(kb + r, a[r], true);
+      for (int r = 0; r < D; ++r) step(kb + r, a[r][0], true);
     }
     // tail of nkb % D blocks, straight-line (ring slot r holds block kb + r)
 #pragma unroll
     for (int r = 0; r < D - 1; ++r)
-      if (kb + r < nkb) step(kb + r, a[r], false);
+      if (kb + r < nkb) step(kb + r, a[r][0], false);
     return;
   }
   f4 a[NT];
@@ -423,6 +558,22 @@ __device__ __forceinline__ void gemm_lds(const T* __restrict__ W, int ldw, int n
   }
 }
 
+// gemm_run with a weight ring: `pre` was filled by the caller (ring_fill before the previous epilogue), else a local
+// one is filled here. (Two call paths, no pointer select, so the ring stays in registers.)
+template <typename T, int NT, int MT>
+__device__ __forceinline__ void gemm_lds(const typename Cfg<T>::w_t* __restrict__ W, int64_t wplane, int ldw, int nrow0,
+                                         const typename Cfg<T>::lds_t* act, int kc0, int nkb, f4 (&acc)[NT][MT],
+                                         int lane, const float* __restrict__ bias = nullptr,
+                                         ARing<T, NT>* pre = nullptr) {
+  if (pre) {
+    gemm_run<T, NT, MT>(W, wplane, ldw, nrow0, act, kc0, nkb, acc, lane, bias, *pre);
+  } else {
+    ARing<T, NT> own;
+    ring_fill<T, NT>(own, W, wplane, ldw, nrow0, nkb, lane);
+    gemm_run<T, NT, MT>(W, wplane, ldw, nrow0, act, kc0, nkb, acc, lane, bias, own);
+  }
+}
+
 // ---- epilogue helpers on a "packed tile": features n..n+3 of one point (one accumulator lane) in storage form.
 // fp32: the f4 itself; bf16: two u32 words (x | y << 16, z | w << 16) from two v_cvt_pk_bf16_f32.
 // ReLU is an integer max with 0 on the stored bits (negative floats / bf16 are negative integers, +0 stays 0),
@@ -434,6 +585,7 @@ typedef unsigned short u2 __attribute__((ext_vector_type(2)));
 template <typename T> struct Pk;
 template <> struct Pk<float> { f4 v; };
 template <> struct Pk<bf16_t> { uint32_t w0, w1; };
+template <> struct Pk<x3_t> { f4 v; };  // kept in fp32; split into the three LDS planes when written
 
 template <typename T> __device__ __forceinline__ Pk<T> pk_make(f4 v);
 template <> __device__ __forceinline__ Pk<float> pk_make<float>(f4 v) { return Pk<float>{v}; }
@@ -441,6 +593,7 @@ template <> __device__ __forceinline__ Pk<bf16_t> pk_make<bf16_t>(f4 v) {
   const bh2 lo = __builtin_convertvector(f2{v.x, v.y}, bh2), hi = __builtin_convertvector(f2{v.z, v.w}, bh2);
   return Pk<bf16_t>{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
 }
+template <> __device__ __forceinline__ Pk<x3_t> pk_make<x3_t>(f4 v) { return Pk<x3_t>{v}; }
 template <typename T> __device__ __forceinline__ Pk<T> pk_relu(Pk<T> p);
 template <> __device__ __forceinline__ Pk<float> pk_relu<float>(Pk<float> p) {
   f4 r;
@@ -449,6 +602,9 @@ template <> __device__ __forceinline__ Pk<float> pk_relu<float>(Pk<float> p) {
   r.z = __int_as_float(max(__float_as_int(p.v.z), 0));
   r.w = __int_as_float(max(__float_as_int(p.v.w), 0));
   return Pk<float>{r};
+}
+template <> __device__ __forceinline__ Pk<x3_t> pk_relu<x3_t>(Pk<x3_t> p) {
+  return Pk<x3_t>{pk_relu<float>(Pk<float>{p.v}).v};
 }
 template <> __device__ __forceinline__ Pk<bf16_t> pk_relu<bf16_t>(Pk<bf16_t> p) {
   const s2 z = {0, 0};
@@ -462,6 +618,7 @@ template <> __device__ __forceinline__ uint32_t pk_bits<float>(Pk<float> p) {
                  b2 = min(__float_as_uint(p.v.z), 1u), b3 = min(__float_as_uint(p.v.w), 1u);
   return b0 | (b1 << 1) | (b2 << 2) | (b3 << 3);
 }
+template <> __device__ __forceinline__ uint32_t pk_bits<x3_t>(Pk<x3_t> p) { return pk_bits<float>(Pk<float>{p.v}); }
 template <> __device__ __forceinline__ uint32_t pk_bits<bf16_t>(Pk<bf16_t> p) {
   const u2 one = {1, 1};
   const uint32_t m0 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u2, p.w0), one));
@@ -470,7 +627,7 @@ template <> __device__ __forceinline__ uint32_t pk_bits<bf16_t>(Pk<bf16_t> p) {
   return (t & 5u) | ((t >> 15) & 10u);
 }
 // write the packed tile to LDS row m, features n..n+3
-template <typename T> __device__ __forceinline__ void pk_lds(T* act, int m, int n, Pk<T> p);
+template <typename T> __device__ __forceinline__ void pk_lds(typename Cfg<T>::lds_t* act, int m, int n, Pk<T> p);
 template <> __device__ __forceinline__ void pk_lds<float>(float* act, int m, int n, Pk<float> p) {
   *(f4*)(act + m * ROW + swz<float>(m, n / 4) * 4) = p.v;
 }
@@ -478,8 +635,23 @@ template <> __device__ __forceinline__ void pk_lds<bf16_t>(bf16_t* act, int m, i
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   *(u32x2*)(act + m * ROW + swz<bf16_t>(m, n / 8) * 8 + (n & 7)) = u32x2{p.w0, p.w1};
 }
+template <> __device__ __forceinline__ void pk_lds<x3_t>(bf16_t* act, int m, int n, Pk<x3_t> p) {
+  // v = t0 + t1 + t2 per element, each plane packed pairwise (v_cvt_pk_bf16_f32) like the bf16 tile
+  constexpr int PL = Cfg<x3_t>::M * ROW;
+  const f4 v0 = p.v;
+  const Pk<bf16_t> h0 = pk_make<bf16_t>(v0);
+  const f4 r1 = v0 - f4{__uint_as_float(h0.w0 << 16), __uint_as_float(h0.w0 & 0xffff0000u),
+                        __uint_as_float(h0.w1 << 16), __uint_as_float(h0.w1 & 0xffff0000u)};
+  const Pk<bf16_t> h1 = pk_make<bf16_t>(r1);
+  const f4 r2 = r1 - f4{__uint_as_float(h1.w0 << 16), __uint_as_float(h1.w0 & 0xffff0000u),
+                        __uint_as_float(h1.w1 << 16), __uint_as_float(h1.w1 & 0xffff0000u)};
+  const Pk<bf16_t> h2 = pk_make<bf16_t>(r2);
+  pk_lds<bf16_t>(act, m, n, h0);
+  pk_lds<bf16_t>(act + PL, m, n, h1);
+  pk_lds<bf16_t>(act + 2 * PL, m, n, h2);
+}
 // store the packed tile into 4 consecutive feature-major rows (stride ld)
-template <typename T> __device__ __forceinline__ void pk_store_rows(T* dst, int64_t ld, Pk<T> p);
+template <typename T> __device__ __forceinline__ void pk_store_rows(typename Cfg<T>::st_t* dst, int64_t ld, Pk<T> p);
 // Plain stores: the scattered 2-/4-byte row segments rely on write-combining in L2 (measured: non-temporal
 // stores made the bf16 forward 2.6x slower).
 template <typename V> __device__ __forceinline__ void st_stream(V* p, V v) { *p = v; }
@@ -488,6 +660,9 @@ template <> __device__ __forceinline__ void pk_store_rows<float>(float* dst, int
   st_stream(dst + ld, p.v.y);
   st_stream(dst + 2 * ld, p.v.z);
   st_stream(dst + 3 * ld, p.v.w);
+}
+template <> __device__ __forceinline__ void pk_store_rows<x3_t>(float* dst, int64_t ld, Pk<x3_t> p) {
+  pk_store_rows<float>(dst, ld, Pk<float>{p.v});
 }
 template <> __device__ __forceinline__ void pk_store_rows<bf16_t>(bf16_t* dst, int64_t ld, Pk<bf16_t> p) {
   st_stream(dst, (bf16_t)p.w0);
@@ -508,15 +683,18 @@ __device__ __forceinline__ f4 apply_mask4(f4 v, uint64_t bits, int sh) {
 
 // Harmonic embedding (models/utils.py:98-102) of 3-vector x: columns [sin(x_i 2^f) i-major f-minor | cos(...) | x],
 // zero-padded to `width`, written into LDS row m at column col0 (and, when `sv` is set, into feature-major saved
-// rows sv[k * ld]). The 4 threads of a point share the work: thread q takes the (i, f) pairs j = q, q+4, ...
+// rows sv[k * ld]). The TPP threads of a point share the work: thread q takes the (i, f) pairs j = q, q+TPP, ...
 // and one sincosf per pair yields both the sin column j and the cos column 3F + j.
 template <typename T>
-__device__ __forceinline__ void harmonic_to_lds(T* act, int m, int col0, int width, const float x[3], int F,
-                                                int append, int q, T* sv, int64_t ld) {
-  if constexpr (sizeof(T) == 2) {
+__device__ __forceinline__ void harmonic_to_lds(typename Cfg<T>::lds_t* act, int m, int col0, int width,
+                                                const float x[3], int F, int append, int q,
+                                                typename Cfg<T>::st_t* sv, int64_t ld) {
+  constexpr int TPP = Cfg<T>::WAVES * 64 / Cfg<T>::M;
+  if constexpr (!is_x3<T> && sizeof(T) == 2) {
     // bf16 mode: thread q < 3 takes coordinate q at every frequency with the hardware sin/cos of the angle
     // reduced to revolutions (|error| ~1e-4 rad at the top frequency, far below the bf16 rounding of the value);
     // thread 3 writes [x, zero padding]
+    static_assert(TPP == 4, "bf16 harmonic split");
     if (q < 3) {
       const float xi = q == 0 ? x[0] : (q == 1 ? x[1] : x[2]);
       const float r0 = xi * 0.15915494309189535f;
@@ -524,11 +702,11 @@ __device__ __forceinline__ void harmonic_to_lds(T* act, int m, int col0, int wid
         const float r = __builtin_amdgcn_fractf(r0 * (float)(1 << f));
         const float sn = __builtin_amdgcn_sinf(r), cs = __builtin_amdgcn_cosf(r);
         const int j = q * F + f;
-        act[lds_idx<T>(m, col0 + j)] = to_t<T>(sn);
-        act[lds_idx<T>(m, col0 + 3 * F + j)] = to_t<T>(cs);
+        lds_put1<T>(act, m, col0 + j, sn);
+        lds_put1<T>(act, m, col0 + 3 * F + j, cs);
         if (sv) {
-          sv[(int64_t)j * ld] = to_t<T>(sn);
-          sv[(int64_t)(3 * F + j) * ld] = to_t<T>(cs);
+          sv[(int64_t)j * ld] = to_st<T>(sn);
+          sv[(int64_t)(3 * F + j) * ld] = to_st<T>(cs);
         }
       }
     } else {
@@ -538,49 +716,34 @@ __device__ __forceinline__ void harmonic_to_lds(T* act, int m, int col0, int wid
         v = a == 1 ? x[1] : v;
         v = a == 2 ? x[2] : v;
         v = append ? v : 0.0f;
-        act[lds_idx<T>(m, col0 + k)] = to_t<T>(v);
-        if (sv) sv[(int64_t)k * ld] = to_t<T>(v);
+        lds_put1<T>(act, m, col0 + k, v);
+        if (sv) sv[(int64_t)k * ld] = to_st<T>(v);
       }
     }
     return;
   }
-  for (int j = q; j < 3 * F; j += 4) {
+  for (int j = q; j < 3 * F; j += TPP) {
     const int i = j / F, f = j - i * F;
     float xi = x[0];
     xi = i == 1 ? x[1] : xi;
     xi = i == 2 ? x[2] : xi;
     float sn, cs;
-    sincosf(xi * (float)(1 << f), &sn, &cs);  // the parity mode keeps libm-accurate sin/cos
-    act[lds_idx<T>(m, col0 + j)] = to_t<T>(sn);
-    act[lds_idx<T>(m, col0 + 3 * F + j)] = to_t<T>(cs);
+    sincosf(xi * (float)(1 << f), &sn, &cs);  // the fp32 modes keep libm-accurate sin/cos
+    lds_put1<T>(act, m, col0 + j, sn);
+    lds_put1<T>(act, m, col0 + 3 * F + j, cs);
     if (sv) {
-      sv[(int64_t)j * ld] = to_t<T>(sn);
-      sv[(int64_t)(3 * F + j) * ld] = to_t<T>(cs);
+      sv[(int64_t)j * ld] = to_st<T>(sn);
+      sv[(int64_t)(3 * F + j) * ld] = to_st<T>(cs);
     }
   }
-  for (int k = 6 * F + q; k < width; k += 4) {
+  for (int k = 6 * F + q; k < width; k += TPP) {
     const int a = k - 6 * F;
     float v = a == 0 ? x[0] : 0.0f;
     v = a == 1 ? x[1] : v;
     v = a == 2 ? x[2] : v;
     v = append ? v : 0.0f;
-    act[lds_idx<T>(m, col0 + k)] = to_t<T>(v);
-    if (sv) sv[(int64_t)k * ld] = to_t<T>(v);
-  }
-}
-
-// dot of `w[0..NK)` with LDS row m, columns [k0, k0 + NK) (k0 a multiple of the chunk width), summed in column order
-template <typename T> __device__ __forceinline__ void unpack_chunk(f4 raw, float (&v)[Cfg<T>::EPC]);
-template <> __device__ __forceinline__ void unpack_chunk<float>(f4 raw, float (&v)[4]) {
-  v[0] = raw.x; v[1] = raw.y; v[2] = raw.z; v[3] = raw.w;
-}
-template <> __device__ __forceinline__ void unpack_chunk<bf16_t>(f4 raw, float (&v)[8]) {
-  const uint32_t w[4] = {__float_as_uint(raw.x), __float_as_uint(raw.y), __float_as_uint(raw.z),
-                         __float_as_uint(raw.w)};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    lds_put1<T>(act, m, col0 + k, v);
+    if (sv) sv[(int64_t)k * ld] = to_st<T>(v);
   }
 }
 
@@ -594,23 +757,25 @@ __device__ __forceinline__ void store_mask_tile(uint64_t* masks, int64_t Npad, i
 // ============================================================================================ forward
 template <typename T>
 __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_fwd_kernel(
-    MlpLayout lay, const T* __restrict__ Wt, const float* __restrict__ Wf, const float* __restrict__ origins,
-    const float* __restrict__ dirs, const float* __restrict__ lengths, int64_t R, int64_t P,
-    float* __restrict__ sigma, float* __restrict__ rgb, T* __restrict__ saved, uint64_t* __restrict__ masks,
-    int64_t Npad) {
+    MlpLayout lay, const typename Cfg<T>::w_t* __restrict__ Wt, const float* __restrict__ Wf,
+    const float* __restrict__ origins, const float* __restrict__ dirs, const float* __restrict__ lengths, int64_t R,
+    int64_t P, float* __restrict__ sigma, float* __restrict__ rgb, typename Cfg<T>::st_t* __restrict__ saved,
+    uint64_t* __restrict__ masks, int64_t Npad) {
   constexpr int M = Cfg<T>::M, WAVES = Cfg<T>::WAVES, MT = M / 16;
   constexpr int NT = 256 / 16 / WAVES, NTC = HC / 16 / WAVES;
-  constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
-  static_assert(M * 4 == WAVES * 64, "4 threads per point");
-  static_assert(NT * MT == 16, "per-lane mask word holds 16 tiles x 4 bits");
-  __shared__ __attribute__((aligned(16))) T act[M * ROW];
+  constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB, TPP = WAVES * 64 / M;  // threads per point
+  static_assert(NT * MT <= 16, "per-lane mask word holds at most 16 tiles x 4 bits");
+  static_assert(MT <= WAVES, "one wave per 16-point group in the heads");
+  typedef typename Cfg<T>::lds_t LT;
+  __shared__ __attribute__((aligned(16))) LT act[Cfg<T>::PLANES * M * ROW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int64_t N = R * P;
   const int64_t p0 = (int64_t)blockIdx.x * M;
-  const int64_t ld = row_ld(Npad, sizeof(T));
+  const int64_t ld = row_ld(Npad, sizeof(typename Cfg<T>::st_t));
+  const int64_t wpl = lay.t_plane;
   const SavedRows SR = saved_rows(lay.L);
-  const int mt_ = tid >> 2, q = tid & 3;
+  const int mt_ = tid / TPP, q = tid % TPP;
   const int64_t p = p0 + mt_;
   const int64_t pc = p < N ? p : N - 1;
   const int64_t ray = pc / P;
@@ -633,14 +798,16 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   const int nrow0 = wave * NT * 16;
   // weight ring of the next GEMM, filled before the current layer's epilogue (bf16; no-op for fp32)
   ARing<T, NT> ring;
-  ring_fill<T, NT>(ring, Wt + lay.w_off[0], lay.kpad[0], nrow0, KPE / KB, lane);
+  ring_fill<T, NT>(ring, Wt + lay.w_off[0], wpl, lay.kpad[0], nrow0, KPE / KB, lane);
   for (int l = 0; l < lay.L; ++l) {
     const bool sk = (lay.skip >> l) & 1u;
     const int kc0 = (l == 0) ? PE_COL / EPC : 0;
     const int nkb = (l == 0) ? KPE / KB : (sk ? 320 / KB : 256 / KB);
-    gemm_lds<T, NT, MT>(Wt + lay.w_off[l], lay.kpad[l], nrow0, act, kc0, nkb, acc, lane, Wf + lay.b_off[l], &ring);
-    if (l + 1 < lay.L) ring_fill<T, NT>(ring, Wt + lay.w_off[l + 1], lay.kpad[l + 1], nrow0, lay.kpad[l + 1] / KB, lane);
-    else ring_fill<T, NT>(ring, Wt + lay.wint_off, 256, nrow0, 256 / KB, lane);
+    gemm_lds<T, NT, MT>(Wt + lay.w_off[l], wpl, lay.kpad[l], nrow0, act, kc0, nkb, acc, lane, Wf + lay.b_off[l],
+                        &ring);
+    if (l + 1 < lay.L)
+      ring_fill<T, NT>(ring, Wt + lay.w_off[l + 1], wpl, lay.kpad[l + 1], nrow0, lay.kpad[l + 1] / KB, lane);
+    else ring_fill<T, NT>(ring, Wt + lay.wint_off, wpl, 256, nrow0, 256 / KB, lane);
     if (!(YANERF_ABLATE & 32)) __syncthreads();
     uint64_t bits = 0;
 #pragma unroll
@@ -651,7 +818,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
         const Pk<T> h = pk_relu<T>(pk_make<T>(acc[nt][mt]));
         const int m = 16 * mt + li;
         if (!(YANERF_ABLATE & 16)) pk_lds<T>(act, m, n, h);
-        else if (__float_as_uint(acc[nt][mt].x) == 0x7fc00001u) act[m] = (T)0;  // keep acc live
+        else if (__float_as_uint(acc[nt][mt].x) == 0x7fc00001u) act[m] = (LT)0;  // keep acc live
         if (saved && !(YANERF_ABLATE & 4)) {
           pk_store_rows<T>(saved + (SR.h0 + 256LL * l + n) * ld + p0 + m, ld, h);
           bits |= (uint64_t)pk_bits<T>(h) << ((nt * MT + mt) * 4);
@@ -665,16 +832,16 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   // wave over its 16 points (rows past 0 are zero weights); lanes g == 0 hold sigma of point 16 * wave + li.
   // Shifting the LDS base by 16 * wave rows keeps the row swizzle (it depends on the row mod 16).
   float sig = 0.f;
-  if (!(YANERF_ABLATE & 8)) {
+  if (!(YANERF_ABLATE & 8) && wave < MT) {
     f4 hacc[1][1];
-    gemm_lds<T, 1, 1>(Wt + lay.wdh_off, 256, 0, act + 16 * wave * ROW, 0, 256 / KB, hacc, lane);
+    gemm_lds<T, 1, 1>(Wt + lay.wdh_off, wpl, 256, 0, act + 16 * wave * ROW, 0, 256 / KB, hacc, lane);
     sig = hacc[0][0].x + Wf[lay.bd_off];
   }
   // ---- intermediate_linear (no activation)
-  gemm_lds<T, NT, MT>(Wt + lay.wint_off, 256, nrow0, act, 0, 256 / KB, acc, lane, Wf + lay.bint_off, &ring);
+  gemm_lds<T, NT, MT>(Wt + lay.wint_off, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, Wf + lay.bint_off, &ring);
   const int crow0 = wave * NTC * 16;
   ARing<T, NTC> ringc;
-  ring_fill<T, NTC>(ringc, Wt + lay.wc_off, KC, crow0, KC / KB, lane);
+  ring_fill<T, NTC>(ringc, Wt + lay.wc_off, wpl, KC, crow0, KC / KB, lane);
   __syncthreads();
   {
 #pragma unroll
@@ -702,7 +869,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   // ---- color layer: LinearWithRepeat(256 + 27 -> 128) + ReLU as one K = 288 GEMM over [Y, dirPE]
   {
     f4 accc[NTC][MT];
-    gemm_lds<T, NTC, MT>(Wt + lay.wc_off, KC, crow0, act, 0, KC / KB, accc, lane, Wf + lay.bc_off, &ringc);
+    gemm_lds<T, NTC, MT>(Wt + lay.wc_off, wpl, KC, crow0, act, 0, KC / KB, accc, lane, Wf + lay.bc_off, &ringc);
     __syncthreads();
 #pragma unroll
     for (int nt = 0; nt < NTC; ++nt) {
@@ -716,7 +883,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
         pk_lds<T>(act, m, n, h);
         if (saved) {
           pk_store_rows<T>(saved + (SR.c + n) * ld + p0 + m, ld, h);
-          store_mask_tile(masks + (int64_t)lay.L * mask_words_per_slot(Npad), Npad, 0, p0 / 16 + mt,
+          store_mask_tile(masks + (int64_t)lay.L * trunk_mask_words<T>(Npad), Npad, 0, p0 / 16 + mt,
                           (crow0 + 16 * nt) / 16, v, lane);
         }
       }
@@ -726,10 +893,10 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   // ---- output layer 128 -> color_dim + sigmoid, as for the density head (nerf_mlp.py:169-171)
   {
     f4 hacc[1][1] = {{f4{0.f, 0.f, 0.f, 0.f}}};
-    if (!(YANERF_ABLATE & 8))
-      gemm_lds<T, 1, 1>(Wt + lay.woh_off, HC, 0, act + 16 * wave * ROW, 0, HC / KB, hacc, lane);
+    if (!(YANERF_ABLATE & 8) && wave < MT)
+      gemm_lds<T, 1, 1>(Wt + lay.woh_off, wpl, HC, 0, act + 16 * wave * ROW, 0, HC / KB, hacc, lane);
     const int64_t pw = p0 + 16 * wave + li;
-    if (g == 0 && pw < N) {
+    if (wave < MT && g == 0 && pw < N) {
       sigma[pw] = sig;
       const float u[CMAX] = {hacc[0][0].x, hacc[0][0].y, hacc[0][0].z, hacc[0][0].w};
 #pragma unroll
@@ -746,20 +913,23 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
 // ============================================================================================ backward dX
 template <typename T>
 __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_bwd_dx_kernel(
-    MlpLayout lay, const T* __restrict__ Wt, const float* __restrict__ Wf, const T* __restrict__ saved,
+    MlpLayout lay, const typename Cfg<T>::w_t* __restrict__ Wt, const float* __restrict__ Wf,
     const uint64_t* __restrict__ masks, const float* __restrict__ rgb, const float* __restrict__ g_sigma,
-    const float* __restrict__ g_rgb, int64_t N, int64_t Npad, T* __restrict__ grad) {
+    const float* __restrict__ g_rgb, int64_t N, int64_t Npad, typename Cfg<T>::st_t* __restrict__ grad) {
   constexpr int M = Cfg<T>::M, WAVES = Cfg<T>::WAVES, MT = M / 16;
   constexpr int NT = 256 / 16 / WAVES;
-  constexpr int KB = Cfg<T>::KB;
-  __shared__ __attribute__((aligned(16))) T act[M * ROW];
+  constexpr int KB = Cfg<T>::KB, TPP = WAVES * 64 / M, CPT = HC / TPP;  // colour columns per thread
+  static_assert(CPT % 16 == 0, "colour-head backward: whole 16-feature tiles per thread");
+  typedef typename Cfg<T>::lds_t LT;
+  __shared__ __attribute__((aligned(16))) LT act[Cfg<T>::PLANES * M * ROW];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int64_t p0 = (int64_t)blockIdx.x * M;
-  const int64_t ld = row_ld(Npad, sizeof(T));
+  const int64_t ld = row_ld(Npad, sizeof(typename Cfg<T>::st_t));
+  const int64_t wpl = lay.t_plane;
   const GradRows GR = grad_rows(lay.L);
-  const int mt_ = tid >> 2, q = tid & 3;
+  const int mt_ = tid / TPP, q = tid % TPP;
   const int64_t p = p0 + mt_;
   const bool valid = p < N;
   const int cd = lay.cdim;
@@ -773,36 +943,37 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     }
   }
   if (q == 0) {
-    for (int j = 0; j < cd; ++j) grad[(GR.du + j) * ld + p] = to_t<T>(du[j]);
-    grad[(GR.dyx + 256) * ld + p] = to_t<T>(gs);
+    for (int j = 0; j < cd; ++j) grad[(GR.du + j) * ld + p] = to_st<T>(du[j]);
+    grad[(GR.dyx + 256) * ld + p] = to_st<T>(gs);
   }
   {
     const float* wo = Wf + lay.wo_off;
-    // colour-hidden ReLU masks for this point: feature tiles 2q, 2q+1 (slot L)
-    uint64_t cw[2][4];
+    // colour-hidden ReLU masks for this point: feature tiles CPT/16 * q .. (slot L)
+    constexpr int TT = CPT / 16;
+    uint64_t cw[TT][4];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < TT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        cw[t][r] = masks[lay.L * mask_words_per_slot(Npad) + mask_index(Npad, 0, p / 16, 2 * q + t) + r];
-    for (int c = 32 * q; c < 32 * q + 32; ++c) {
+        cw[t][r] = masks[lay.L * trunk_mask_words<T>(Npad) + mask_index(Npad, 0, p / 16, TT * q + t) + r];
+    for (int c = CPT * q; c < CPT * q + CPT; ++c) {
       float dc = 0.0f;
       for (int j = 0; j < cd; ++j) dc += du[j] * wo[j * HC + c];
       const int cl = c & 15;  // feature within its 16-feature tile: ballot word cl & 3, bit 16 * (cl >> 2) + point
-      const uint64_t word = cw[(c >> 4) & 1][cl & 3];
+      const uint64_t word = cw[(c - CPT * q) >> 4][cl & 3];
       const bool on = (word >> (16 * (cl >> 2) + (mt_ & 15))) & 1ull;
       float dz = on ? dc : 0.0f;
-      act[lds_idx<T>(mt_, c)] = to_t<T>(dz);
-      grad[(GR.dzc + c) * ld + p] = to_t<T>(dz);
+      lds_put1<T>(act, mt_, c, dz);
+      grad[(GR.dzc + c) * ld + p] = to_st<T>(dz);
     }
   }
   __syncthreads();
   f4 acc[NT][MT];
   const int nrow0 = wave * NT * 16;
   // ---- dY = Wc[:, :256]^T dZc   (K = 128)
-  gemm_lds<T, NT, MT>(Wt + lay.wcT_off, HC, nrow0, act, 0, HC / KB, acc, lane);
+  gemm_lds<T, NT, MT>(Wt + lay.wcT_off, wpl, HC, nrow0, act, 0, HC / KB, acc, lane);
   ARing<T, NT> ring;  // next GEMM's weights, fetched during the epilogue (bf16)
-  ring_fill<T, NT>(ring, Wt + lay.wintT_off, 256, nrow0, 256 / KB, lane);
+  ring_fill<T, NT>(ring, Wt + lay.wintT_off, wpl, 256, nrow0, 256 / KB, lane);
   __syncthreads();
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
@@ -820,11 +991,11 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   // ---- dH_{L-1} = Wint^T dY + w_d (x) dsigma ; dZ_{L-1} = dH * [H_{L-1} > 0]
   for (int l = lay.L; l >= 1; --l) {
     // l == L: the heads -> last trunk layer; else trunk layer l -> layer l-1
-    const T* A = (l == lay.L) ? Wt + lay.wintT_off : Wt + lay.wt_off[l];
+    const typename Cfg<T>::w_t* A = (l == lay.L) ? Wt + lay.wintT_off : Wt + lay.wt_off[l];
     const int hl = l - 1;  // layer whose output gradient we form
     const uint64_t bits = masks[(((int64_t)hl * gridDim.x + blockIdx.x) * WAVES + wave) * 64 + lane];
-    gemm_lds<T, NT, MT>(A, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring);
-    if (l - 1 >= 1) ring_fill<T, NT>(ring, Wt + lay.wt_off[l - 1], 256, nrow0, 256 / KB, lane);
+    gemm_lds<T, NT, MT>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring);
+    if (l - 1 >= 1) ring_fill<T, NT>(ring, Wt + lay.wt_off[l - 1], wpl, 256, nrow0, 256 / KB, lane);
     __syncthreads();
     const float* wd = Wf + lay.wd_off;
 #pragma unroll
@@ -884,7 +1055,11 @@ struct DwJobs {
 constexpr int DW_THREADS = 512;
 // widest dW column tile: bf16 is HBM/L2-bound (a 256-wide tile reads each dZ row once), fp32 is MFMA-bound and
 // runs faster with 128-wide tiles (measured: fp32 dW 8.3 ms vs 11.0 ms at 256; bf16 1.66 vs 2.0 ms at 128)
-__host__ __device__ constexpr int dw_bkmax(int prec) { return prec == YANERF_PREC_F32 ? 128 : 256; }
+__host__ __device__ constexpr int dw_bkmax(int prec) { return prec == YANERF_PREC_BF16 ? 256 : 128; }
+template <typename T> constexpr int prec_of = YANERF_PREC_BF16;
+template <> constexpr int prec_of<float> = YANERF_PREC_F32;
+template <> constexpr int prec_of<x3_t> = YANERF_PREC_F32X3;
+
 
 template <typename T> __device__ __forceinline__ float hsum16(f4 v);
 template <> __device__ __forceinline__ float hsum16<float>(f4 v) { return (v.x + v.y) + (v.z + v.w); }
@@ -912,6 +1087,12 @@ constexpr int DW_CPR = YANERF_DW_CPR;      // 16-byte chunks per staged row (4: 
 constexpr int DW_RB = 16 * DW_CPR;          // staged row bytes
 constexpr int DW_RPI = 64 / DW_CPR;         // rows per DMA wave-instruction
 constexpr int DW_STAGES = DW_CPR == 4 ? 4 : 2, DW_STAGE_BYTES = 512 * DW_RB;
+// points per dW stage: one K-block of the dW MFMA per staged row (x3: always one bf16 K-block, register staged)
+constexpr int X3_SPTS = 32;
+static int64_t dw_stage_pts(int prec) {
+  if (prec == YANERF_PREC_F32X3) return X3_SPTS;
+  return (prec == YANERF_PREC_F32 ? Cfg<float>::KB : Cfg<bf16_t>::KB) * (DW_CPR / 4);
+}
 __device__ __forceinline__ int dw_swz(int row, int c) {
   return DW_CPR == 4 ? (c ^ (((row >> 3) & 1) << 1)) : (c ^ ((row >> 1) & 7));
 }
@@ -1052,9 +1233,145 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
   }
 }
 
+// x3 dW: dZ and the layer inputs are fp32 rows in HBM (the x3 forward / dX save fp32). Each stage of 32 points is
+// loaded with 16-byte register loads (4 points of one row per thread-load, the next stage in flight while the
+// current one multiplies), split into three bf16 planes on the way into LDS (same 64-byte rows and swizzle as the
+// bf16 dW tile) and multiplied with the six plane products per 16x16x32 step. Two LDS buffers, one barrier per
+// stage. Bias gradients are fp32 row sums of the loaded dZ segments.
+template <int BN, int BK>
+__device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S, int64_t Npad,
+                                           float* __restrict__ slab, int64_t slab_elems, char* smem) {
+  constexpr int WN = BN / 64, WK0 = 8 / WN, WK = (BK / 16 < WK0) ? BK / 16 : WK0, KTW = BK / WK / 16;
+  static_assert(KTW >= 1 && WN * WK <= 8, "dW wave tiling");
+  constexpr int ROWS = BN + BK, LPT = (ROWS * 8 + DW_THREADS - 1) / DW_THREADS;  // 16-B loads per thread per stage
+  constexpr int PLB = 384 * 64, BUFB = 3 * PLB;                                  // plane / buffer bytes
+  static_assert(ROWS <= 384, "x3 dW staging: at most 384 rows");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int wn = wave / WK, wk = wave % WK;
+  const bool mma_wave = wave < WN * WK;
+  const int64_t nst = Npad / X3_SPTS, ld = row_ld(Npad, sizeof(float));
+  const int64_t st_lo = nst * s / S, st_hi = nst * (s + 1) / S;
+  const float* src[LPT];
+  int dst[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) {
+    const int flat = tid + DW_THREADS * i, row = flat >> 3, seg = flat & 7;
+    const float* p;
+    if (row < BN) {
+      p = (const float*)J.A + (int64_t)(row < J.a_rows ? row : 0) * ld;
+    } else {
+      const int k = k0 + row - BN;
+      if (k < J.x0_rows) p = (const float*)J.X0 + (int64_t)k * ld;
+      else if (k < J.ktot) p = (const float*)J.X1 + (int64_t)(k - J.x0_rows) * ld;
+      else p = (const float*)J.X0;
+    }
+    src[i] = p + seg * 4;
+    dst[i] = row < ROWS ? row * 64 + (dw_swz(row, seg >> 1) << 4) + (seg & 1) * 8 : -1;
+  }
+  f4 regs[LPT];
+  auto load = [&](int64_t st) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) regs[i] = *(const f4*)(src[i] + st * X3_SPTS);
+  };
+  float rsum[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) rsum[i] = 0.f;
+  const bool do_bias = (k0 == 0);
+  const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
+  f4 acc[4][KTW];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int q = 0; q < KTW; ++q) acc[nt][q] = zero;
+  if (st_lo < st_hi) load(st_lo);
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  for (int64_t st = st_lo; st < st_hi; ++st) {
+    char* buf = smem + (int)(st & 1) * BUFB;
+    // split the staged fp32 segments into the three planes of this stage's buffer
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      if (dst[i] >= 0) {
+        const f4 v0 = regs[i];
+        if (do_bias && (tid + DW_THREADS * i) / 8 < BN) rsum[i] += (v0.x + v0.y) + (v0.z + v0.w);
+        const Pk<bf16_t> h0 = pk_make<bf16_t>(v0);
+        const f4 r1 = v0 - f4{__uint_as_float(h0.w0 << 16), __uint_as_float(h0.w0 & 0xffff0000u),
+                              __uint_as_float(h0.w1 << 16), __uint_as_float(h0.w1 & 0xffff0000u)};
+        const Pk<bf16_t> h1 = pk_make<bf16_t>(r1);
+        const f4 r2 = r1 - f4{__uint_as_float(h1.w0 << 16), __uint_as_float(h1.w0 & 0xffff0000u),
+                              __uint_as_float(h1.w1 << 16), __uint_as_float(h1.w1 & 0xffff0000u)};
+        const Pk<bf16_t> h2 = pk_make<bf16_t>(r2);
+        *(u32x2*)(buf + dst[i]) = u32x2{h0.w0, h0.w1};
+        *(u32x2*)(buf + PLB + dst[i]) = u32x2{h1.w0, h1.w1};
+        *(u32x2*)(buf + 2 * PLB + dst[i]) = u32x2{h2.w0, h2.w1};
+      }
+    }
+    __syncthreads();
+    if (st + 1 < st_hi) load(st + 1);
+    if (mma_wave) {
+      f4 a[3][4];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int row = wn * 64 + 16 * nt + li;
+          a[pl][nt] = *(const f4*)(buf + pl * PLB + row * 64 + (dw_swz(row, g) << 4));
+        }
+      constexpr int QG = KTW < 4 ? KTW : 4;
+#pragma unroll
+      for (int q0 = 0; q0 < KTW; q0 += QG) {
+        f4 b[3][QG];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+          for (int q = 0; q < QG; ++q) {
+            const int row = BN + (wk * KTW + q0 + q) * 16 + li;
+            b[pl][q] = *(const f4*)(buf + pl * PLB + row * 64 + (dw_swz(row, g) << 4));
+          }
+        constexpr int TI[6] = {2, 1, 0, 1, 0, 0}, TJ[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int q = 0; q < QG; ++q)
+              acc[nt][q0 + q] = mma_blk<bf16_t>(a[TI[t]][nt], b[TJ[t]][q], acc[nt][q0 + q]);
+      }
+    }
+  }
+  float* out = slab + (int64_t)s * slab_elems + J.slab_off;
+  const int kv = J.ktot + 1;
+  if (mma_wave) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int q = 0; q < KTW; ++q) {
+        const int k = k0 + (wk * KTW + q) * 16 + li;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = wn * 64 + 16 * nt + 4 * g + r;
+          if (n < J.a_rows && k < J.ktot) out[(int64_t)n * kv + k] = acc[nt][q][r];
+        }
+      }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int flat = tid + DW_THREADS * i, row = flat >> 3;
+      float v = rsum[i];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      if ((flat & 7) == 0 && row < BN && row < J.a_rows) out[(int64_t)row * kv + J.ktot] = v;
+    }
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t Npad, int S, float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) char smem[DW_STAGES * DW_STAGE_BYTES];
+  // x3: two buffers of three 384-row bf16 planes (144 KB); otherwise the LDS-DMA ring
+  __shared__ __attribute__((aligned(16))) char smem[is_x3<T> ? 2 * 3 * 384 * 64 : DW_STAGES * DW_STAGE_BYTES];
   // 1-D grid in job order (heaviest first); inside a job, split-major so the k-tiles sharing a dZ slab run together
   const int b = blockIdx.x;
   int ji = 0;
@@ -1062,11 +1379,21 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   const DwJob& J = jobs.j[ji];
   const int local = b - J.tile_base * S;
   const int s = local / J.k_tiles, kt = local % J.k_tiles;
-  constexpr int BKMAX = dw_bkmax(sizeof(T) == 4 ? YANERF_PREC_F32 : YANERF_PREC_BF16);
+  constexpr int BKMAX = dw_bkmax(prec_of<T>);
   const int k0 = kt * BKMAX;
   const int bk = kt < J.k_full ? BKMAX : J.bk_tail;
   const int64_t se = jobs.slab_elems;
-  if (J.bn == 256) {
+  if constexpr (is_x3<T>) {
+    if (J.bn == 256) {
+      if (bk == 128) dw_tile_x3<256, 128>(J, k0, s, S, Npad, slab, se, smem);
+      else dw_tile_x3<256, 64>(J, k0, s, S, Npad, slab, se, smem);
+    } else if (J.bn == 128) {
+      if (bk == 128) dw_tile_x3<128, 128>(J, k0, s, S, Npad, slab, se, smem);
+      else dw_tile_x3<128, 64>(J, k0, s, S, Npad, slab, se, smem);
+    } else {
+      dw_tile_x3<64, 128>(J, k0, s, S, Npad, slab, se, smem);
+    }
+  } else if (J.bn == 256) {
     if (bk == 256) dw_tile<T, 256, 256>(J, k0, s, S, Npad, slab, se, smem);
     else if (bk == 128) dw_tile<T, 256, 128>(J, k0, s, S, Npad, slab, se, smem);
     else dw_tile<T, 256, 64>(J, k0, s, S, Npad, slab, se, smem);
@@ -1220,16 +1547,19 @@ static int64_t dw_slab_elems_for(const MlpLayout& L, int prec, int* total_tiles)
   return e;
 }
 
+// dW kernel type and precision per mode: x3 saves fp32 activations / gradients, so its weight gradients run on
+// the exact-fp32 dW kernel
 template <typename T>
-static int launch_fwd(const MlpLayout& L, const void* packed, const float* o, const float* d, const float* t, int64_t R,
-                      int64_t P, float* sigma, float* rgb, void* saved, hipStream_t st) {
+static int launch_fwd(const MlpLayout& L, int prec, const void* packed, const float* o, const float* d, const float* t,
+                      int64_t R, int64_t P, float* sigma, float* rgb, void* saved, hipStream_t st) {
+  typedef typename Cfg<T>::st_t ST;
   const int64_t N = R * P;
-  const int64_t Npad = npad_of(sizeof(T) == 4 ? YANERF_PREC_F32 : YANERF_PREC_BF16, N);
-  const T* Wt = (const T*)packed;
+  const int64_t Npad = npad_of(prec, N);
+  const typename Cfg<T>::w_t* Wt = (const typename Cfg<T>::w_t*)packed;
   const float* Wf = (const float*)((const char*)packed + L.f_base);
   dim3 grid((unsigned)(Npad / Cfg<T>::M)), block(Cfg<T>::WAVES * 64);
-  uint64_t* masks = saved ? (uint64_t*)((char*)saved + saved_t_bytes(L.L, Npad, sizeof(T))) : nullptr;
-  hipLaunchKernelGGL(mlp_fwd_kernel<T>, grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, (T*)saved, masks,
+  uint64_t* masks = saved ? (uint64_t*)((char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST))) : nullptr;
+  hipLaunchKernelGGL(mlp_fwd_kernel<T>, grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, (ST*)saved, masks,
                      Npad);
   YN_LAUNCH_CHECK("mlp_forward");
   return 0;
@@ -1238,20 +1568,21 @@ static int launch_fwd(const MlpLayout& L, const void* packed, const float* o, co
 template <typename T>
 static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const void* saved, const float* rgb,
                       const float* gs, const float* gr, int64_t N, float* const* grads, void* ws, hipStream_t st) {
+  typedef typename Cfg<T>::st_t ST;
   const int64_t Npad = npad_of(prec, N);
-  const T* Wt = (const T*)packed;
+  const typename Cfg<T>::w_t* Wt = (const typename Cfg<T>::w_t*)packed;
   const float* Wf = (const float*)((const char*)packed + L.f_base);
   const GradRows GR = grad_rows(L.L);
-  T* gradbuf = (T*)ws;
-  int64_t grad_bytes = GR.rows * row_ld(Npad, sizeof(T)) * (int64_t)sizeof(T);
+  ST* gradbuf = (ST*)ws;
+  int64_t grad_bytes = GR.rows * row_ld(Npad, sizeof(ST)) * (int64_t)sizeof(ST);
   float* slab = (float*)((char*)ws + grad_bytes);
-  const uint64_t* masks = (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(T)));
+  const uint64_t* masks = (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST)));
   hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::WAVES * 64), 0, st, L, Wt,
-                     Wf, (const T*)saved, masks, rgb, gs, gr, N, Npad, gradbuf);
+                     Wf, masks, rgb, gs, gr, N, Npad, gradbuf);
   YN_LAUNCH_CHECK("mlp_backward_dx");
   DwJobs D;
   build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D);
-  const int S = dw_splits(D.total_tiles, Npad / (Cfg<T>::KB * (DW_CPR / 4)));
+  const int S = dw_splits(D.total_tiles, Npad / dw_stage_pts(prec));
   hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)(D.total_tiles * S)), dim3(DW_THREADS), 0, st, D, Npad, S, slab);
   YN_LAUNCH_CHECK("mlp_backward_dw");
   hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((D.slab_elems + 255) / 256)), dim3(256), 0, st, D, S, slab);
@@ -1277,7 +1608,8 @@ int64_t yanerf_mlp_packed_bytes(const yanerf_mlp_desc* d, int precision) {
 
 int yanerf_mlp_pack(const yanerf_mlp_desc* d, int precision, const float* const* params, void* packed, void* stream) {
   if (check_desc(d)) return 1;
-  YN_CHECK(precision == YANERF_PREC_F32 || precision == YANERF_PREC_BF16, "mlp_pack: bad precision %d", precision);
+  YN_CHECK(precision == YANERF_PREC_F32 || precision == YANERF_PREC_BF16 || precision == YANERF_PREC_F32X3,
+           "mlp_pack: bad precision %d", precision);
   YN_CHECK(params && packed, "mlp_pack: null pointer");
   for (int i = 0; i < num_params(d); ++i) YN_CHECK(params[i], "mlp_pack: parameter %d is null", i);
   MlpLayout L = make_layout(d, precision);
@@ -1287,9 +1619,11 @@ int yanerf_mlp_pack(const yanerf_mlp_desc* d, int precision, const float* const*
   float* fsec = (float*)(base + L.f_base);
   dim3 grid((unsigned)((J.total + 255) / 256)), block(256);
   if (precision == YANERF_PREC_F32)
-    hipLaunchKernelGGL(pack_kernel<float>, grid, block, 0, as_stream(stream), J, (float*)base, fsec);
+    hipLaunchKernelGGL(pack_kernel<float>, grid, block, 0, as_stream(stream), J, (float*)base, fsec, L.t_plane);
+  else if (precision == YANERF_PREC_BF16)
+    hipLaunchKernelGGL(pack_kernel<bf16_t>, grid, block, 0, as_stream(stream), J, (bf16_t*)base, fsec, L.t_plane);
   else
-    hipLaunchKernelGGL(pack_kernel<bf16_t>, grid, block, 0, as_stream(stream), J, (bf16_t*)base, fsec);
+    hipLaunchKernelGGL(pack_kernel<x3_t>, grid, block, 0, as_stream(stream), J, (bf16_t*)base, fsec, L.t_plane);
   YN_LAUNCH_CHECK("mlp_pack");
   return 0;
 }
@@ -1297,7 +1631,8 @@ int yanerf_mlp_pack(const yanerf_mlp_desc* d, int precision, const float* const*
 int64_t yanerf_mlp_saved_bytes(const yanerf_mlp_desc* d, int precision, int64_t n_points) {
   if (check_desc(d)) return -1;
   const int64_t Npad = npad_of(precision, n_points);
-  return saved_t_bytes(d->n_layers, Npad, elem_size(precision)) + (d->n_layers + 1) * mask_words_per_slot(Npad) * 8;
+  return saved_t_bytes(d->n_layers, Npad, elem_size(precision)) +
+         (d->n_layers * trunk_mask_words_prec(precision, Npad) + mask_words_per_slot(Npad)) * 8;
 }
 
 int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, int64_t n_points) {
@@ -1308,8 +1643,7 @@ int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, 
   int64_t grad_bytes = GR.rows * row_ld(Npad, elem_size(precision)) * (int64_t)elem_size(precision);
   int tiles = 0;
   int64_t se = dw_slab_elems_for(L, precision, &tiles);
-  const int64_t kb = precision == YANERF_PREC_F32 ? Cfg<float>::KB : Cfg<bf16_t>::KB;
-  int S = dw_splits(tiles, Npad / (kb * (DW_CPR / 4)));
+  int S = dw_splits(tiles, Npad / dw_stage_pts(precision));
   return grad_bytes + (int64_t)S * se * 4;
 }
 
@@ -1322,9 +1656,14 @@ int yanerf_mlp_forward(const yanerf_mlp_desc* d, int precision, const void* pack
   if (R == 0) return 0;
   MlpLayout L = make_layout(d, precision);
   if (precision == YANERF_PREC_F32)
-    return launch_fwd<float>(L, packed, origins, directions, lengths, R, P, sigma_raw, rgb, saved, as_stream(stream));
+    return launch_fwd<float>(L, precision, packed, origins, directions, lengths, R, P, sigma_raw, rgb, saved,
+                             as_stream(stream));
   if (precision == YANERF_PREC_BF16)
-    return launch_fwd<bf16_t>(L, packed, origins, directions, lengths, R, P, sigma_raw, rgb, saved, as_stream(stream));
+    return launch_fwd<bf16_t>(L, precision, packed, origins, directions, lengths, R, P, sigma_raw, rgb, saved,
+                              as_stream(stream));
+  if (precision == YANERF_PREC_F32X3)
+    return launch_fwd<x3_t>(L, precision, packed, origins, directions, lengths, R, P, sigma_raw, rgb, saved,
+                            as_stream(stream));
   YN_CHECK(false, "mlp_forward: bad precision %d", precision);
 }
 
@@ -1342,6 +1681,9 @@ int yanerf_mlp_backward(const yanerf_mlp_desc* d, int precision, const void* pac
   if (precision == YANERF_PREC_BF16)
     return launch_bwd<bf16_t>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R * P, grads, workspace,
                               as_stream(stream));
+  if (precision == YANERF_PREC_F32X3)
+    return launch_bwd<x3_t>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R * P, grads, workspace,
+                            as_stream(stream));
   YN_CHECK(false, "mlp_backward: bad precision %d", precision);
 }
 

@@ -16,7 +16,7 @@ from ... import _C, ops
 from .builder import MODELS
 from .utils import HarmonicEmbedding, LinearWithRepeat
 
-_PRECISIONS = {"fp32": _C.PREC_F32, "f32": _C.PREC_F32, "bf16": _C.PREC_BF16}
+_PRECISIONS = {"fp32": _C.PREC_F32, "f32": _C.PREC_F32, "bf16": _C.PREC_BF16, "fp32x3": _C.PREC_F32X3}
 
 
 def _xavier_init(linear) -> None:  # nerf_mlp.py:292-296

@@ -373,10 +373,35 @@ def gen_init_checksums(out):
     out["init_checksums"] = d
 
 
+def gen_pipeline_state(out):
+    """The reference NeRFPipeline's state_dict layout (the checkpoint format of scripts/run.py:168-175, 409-414:
+    {"model": pipeline.state_dict(), ...}) for the Lego and Fern configs, and its seeded-initialisation checksums
+    (torch.manual_seed(42) then PIPELINES.build, as run.py:70-73, 149)."""
+    d = {}
+    for tag, cfgfile in (("lego", "configs/nerf/lego.yml"), ("fern", "configs/nerf/fern.yml")):
+        cfg = Config.fromfile(str(REF / cfgfile))
+        torch.manual_seed(42)
+        pipe = PIPELINES.build(cfg.pipeline)
+        sd = pipe.state_dict()
+        names = list(sd.keys())
+        d[f"{tag}_names"] = np.array(names)
+        d[f"{tag}_ndim"] = np.array([sd[k].dim() for k in names], np.int64)
+        d[f"{tag}_shapes"] = np.array([list(sd[k].shape) + [0] * (2 - sd[k].dim()) for k in names], np.int64)
+        d[f"{tag}_sums"] = np.array([sd[k].double().sum().item() for k in names])
+    out["pipeline_state"] = d
+
+
+GENERATORS = (gen_harmonic, gen_raysampler, gen_mlp, gen_raymarcher, gen_sample_pdf, gen_render_eval,
+              gen_train_step, gen_zero_outputer, gen_init_checksums, gen_pipeline_state)
+
+
 def main():
+    """`make_golden.py [name ...]` regenerates only the named generators (e.g. gen_pipeline_state)."""
     out = {}
-    for f in (gen_harmonic, gen_raysampler, gen_mlp, gen_raymarcher, gen_sample_pdf, gen_render_eval,
-              gen_train_step, gen_zero_outputer, gen_init_checksums):
+    want = set(sys.argv[1:])
+    for f in GENERATORS:
+        if want and f.__name__ not in want:
+            continue
         f(out)
         print("generated", f.__name__)
     for name, d in out.items():

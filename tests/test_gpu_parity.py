@@ -393,3 +393,40 @@ def test_chunking_invariance(pkg, golden):
         pipe.chunk_size_grid = 0  # unchunked
         c = pipe(**kw)["rendered_images"]
     assert torch.equal(a, b) and torch.equal(a, c)
+
+
+# ------------------------------------------------------------------------------------------- checkpoints
+def test_trainer_checkpoint_interop(pkg, tmp_path):
+    """The fused trainer writes the reference checkpoint format (run.py:409-414): a registry NeRFPipeline +
+    torch Adam load it, and a fresh trainer resumed from it takes the identical next step."""
+    import yanerf_boot  # noqa: F401
+    from yanerf_amd import checkpoint, ops
+    from yanerf_amd.train import NeRFTrainer
+    from yanerf_amd.utils.config import Config
+    cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml")).pipeline
+    g = torch.Generator().manual_seed(5)
+    image = torch.rand(1, 800, 800, 3, generator=g).to(DEV)
+    from scene import synthetic_pose
+    poses = [torch.from_numpy(synthetic_pose(th, -30.0, 4.0)).float()[None, :3, :4].contiguous().to(DEV)
+             for th in (0.0, 40.0, 80.0)]
+    focal = torch.tensor([1111.111], device=DEV)
+    tr = NeRFTrainer(cfg, precision="fp32", device=DEV, n_rays=256, seed=11)
+    tr.step(poses[0], focal, image)
+    tr.step(poses[1], focal, image)
+    path = checkpoint.save_checkpoint(str(tmp_path), tr, epoch=3)
+    pipe = pkg["PIPELINES"].build(cfg)
+    opt = torch.optim.Adam(pipe.parameters(), lr=1e-3)
+    assert checkpoint.load_checkpoint(path, pipe, opt) == 4
+    ref = tr.pipeline_state_dict()
+    for k, v in pipe.state_dict().items():
+        assert torch.equal(v, ref[k]), k
+    tr2 = NeRFTrainer(cfg, precision="fp32", device=DEV, n_rays=256, seed=99)
+    checkpoint.load_checkpoint(path, tr2)
+    assert tr2.step_count == 2
+    assert torch.equal(tr2.flat.data, tr.flat.data) and torch.equal(tr2.exp_avg_sq, tr.exp_avg_sq)
+    rng = (ops.RNG._seed, ops.RNG._offset)
+    tr.step(poses[2], focal, image)
+    ops.RNG._seed, ops.RNG._offset = rng
+    tr2.step(poses[2], focal, image)
+    torch.cuda.synchronize()
+    assert torch.equal(tr2.flat.data, tr.flat.data)

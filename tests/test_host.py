@@ -98,3 +98,65 @@ def test_huber():
     x = torch.tensor([0.0, 0.01, 1.0])
     ref = (torch.sqrt(torch.clamp(1 + x / 0.03 ** 2, 0) + 1e-4) - 1) * 0.03
     assert torch.allclose(huber(x), ref)
+
+
+@pytest.mark.parametrize("name", ["lego", "fern"])
+def test_pipeline_state_matches_reference(golden, name):
+    """The registry NeRFPipeline's state_dict = the reference pipeline's (its checkpoint 'model' entry, run.py:
+    168-178): same 48 keys in order, same shapes, and torch.manual_seed(42) + build draws the same weights."""
+    g = golden("pipeline_state")
+    torch.manual_seed(42)
+    pipe = PIPELINES.build(Config.fromfile(str(CFG / f"{name}.yml")).pipeline)
+    sd = pipe.state_dict()
+    names = [str(x) for x in g[f"{name}_names"]]
+    assert list(sd.keys()) == names
+    for k, nd, shp in zip(names, g[f"{name}_ndim"], g[f"{name}_shapes"]):
+        assert tuple(sd[k].shape) == tuple(int(x) for x in shp[:nd])
+    sums = np.array([sd[k].double().sum().item() for k in names])
+    np.testing.assert_array_equal(sums, g[f"{name}_sums"])
+
+
+def test_checkpoint_roundtrip_reference_format(tmp_path):
+    from yanerf_amd import checkpoint
+    torch.manual_seed(0)
+    cfg = Config.fromfile(str(CFG / "lego.yml")).pipeline
+    pipe = PIPELINES.build(cfg)
+    opt = torch.optim.Adam(pipe.parameters(), lr=5e-4)
+    for p in pipe.parameters():  # one synthetic optimizer step so the Adam state is populated
+        p.grad = torch.randn_like(p) * 1e-3
+    opt.step()
+    path = checkpoint.save_checkpoint(str(tmp_path), pipe, opt, epoch=7)
+    assert path.endswith("ckpts/ckpts_0007.pth")
+    ck = torch.load(path, weights_only=True)
+    assert set(ck) == {"model", "optimizer", "epoch"} and len(ck["model"]) == 48
+    torch.manual_seed(1)
+    pipe2 = PIPELINES.build(cfg)
+    opt2 = torch.optim.Adam(pipe2.parameters(), lr=1e-3)
+    assert checkpoint.load_checkpoint(path, pipe2, opt2) == 8
+    for (k, a), b in zip(pipe.state_dict().items(), pipe2.state_dict().values()):
+        assert torch.equal(a, b), k
+    s1, s2 = opt.state_dict(), opt2.state_dict()
+    assert s2["param_groups"][0]["lr"] == 5e-4
+    for i in s1["state"]:
+        assert torch.equal(s1["state"][i]["exp_avg_sq"], s2["state"][i]["exp_avg_sq"])
+
+
+def test_adam_state_flat_conversion():
+    """The fused trainer's flat Adam moments <-> torch.optim.Adam.state_dict() (checkpoint.py)."""
+    from yanerf_amd import checkpoint
+    ps = [torch.nn.Parameter(torch.randn(3, 4)), torch.nn.Parameter(torch.randn(5))]
+    opt = torch.optim.Adam(ps, lr=1e-3, betas=(0.8, 0.99))
+    for p in ps:
+        p.grad = torch.randn_like(p)
+    opt.step()
+    opt.step()
+    n = sum(p.numel() for p in ps)
+    m, v = torch.zeros(n), torch.zeros(n)
+    assert checkpoint.adam_state_to_flat(opt.state_dict(), ps, m, v) == 2
+    osd = checkpoint.adam_state_from_flat(ps, m, v, 2, 1e-3, (0.8, 0.99), 1e-8, 0.0)
+    opt2 = torch.optim.Adam(ps, lr=5.0)
+    opt2.load_state_dict(osd)
+    for i in range(2):
+        for key in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(opt.state_dict()["state"][i][key], opt2.state_dict()["state"][i][key])
+    assert opt2.state_dict()["param_groups"][0]["betas"] == (0.8, 0.99)

@@ -195,6 +195,35 @@ class NeRFTrainer:
                                float(self.eps), float(self.weight_decay), self.step_count, st), "yanerf_adam")
         return out
 
+    # --------------------------------------------------------------------------------------- checkpoints
+    def pipeline_state_dict(self) -> Dict[str, torch.Tensor]:
+        """The two models' parameters under the reference NeRFPipeline's keys (checkpoint.py)."""
+        sd = {}
+        for i, m in enumerate(self.models):
+            for k, v in m.state_dict().items():
+                sd[f"implicit_functions.{i}._fn.{k}"] = v.detach().cpu().clone()
+        return sd
+
+    def load_pipeline_state_dict(self, sd: Dict[str, torch.Tensor]):
+        from . import checkpoint
+        for m, msd in zip(self.models, checkpoint.split_pipeline_state(sd, len(self.models))):
+            m.load_state_dict(msd)  # copies into the flat-buffer views (parameters are not re-allocated)
+
+    def optimizer_state_dict(self) -> Dict:
+        from . import checkpoint
+        return checkpoint.adam_state_from_flat(self.params[0] + self.params[1], self.exp_avg, self.exp_avg_sq,
+                                               self.step_count, self.lr, self.betas, self.eps, self.weight_decay)
+
+    def load_optimizer_state_dict(self, osd: Dict):
+        from . import checkpoint
+        step = checkpoint.adam_state_to_flat(osd, self.params[0] + self.params[1], self.exp_avg, self.exp_avg_sq)
+        self.step_count = step or 0
+        g = osd.get("param_groups", [{}])[0]
+        self.lr = float(g.get("lr", self.lr))
+        self.betas = tuple(g.get("betas", self.betas))
+        self.eps = float(g.get("eps", self.eps))
+        self.weight_decay = float(g.get("weight_decay", self.weight_decay))
+
     @staticmethod
     def objective(out: Dict[str, torch.Tensor]) -> torch.Tensor:
         """mse(fine) + mse(coarse) from the per-ray squared errors (device tensor; no host sync)."""

@@ -145,6 +145,50 @@ def test_mlp_bf16_bounds(pkg, golden):
             close(np.linalg.norm(n(p.grad).astype(np.float64)), nn, 0.1 * nn)
 
 
+def test_mlp_bf16_gradients_elementwise(pkg, golden):
+    """bf16 mode, every parameter gradient element against the fp32 reference: relative L2 error per tensor (on the
+    golden's full gradients, or its sampled elements for the large matrices). Catches layout errors in the saved /
+    gradient rows that the norm bound above would miss (a permuted row keeps the norm)."""
+    g = golden("mlp_lego")
+    m, _ = build_mlp(pkg, LEGO_ARCH, int(g["seed"]), precision="bf16")
+    out = m(t(g["origins"]), t(g["directions"]), t(g["lengths"]))
+    m.zero_grad()
+    ((out["rays_densities"] * t(g["g_sigma"])).sum() + (out["rays_features"] * t(g["g_rgb"])).sum()).backward()
+    worst = 0.0
+    for name, p in m.named_parameters():
+        v = n(p.grad).astype(np.float64)
+        if f"grad:{name}" in g:
+            ref = g[f"grad:{name}"].astype(np.float64)
+        else:
+            ref = g[f"gradval:{name}"].astype(np.float64)
+            v = v.reshape(-1)[g[f"gradidx:{name}"]]
+        rel = np.linalg.norm(v - ref) / max(np.linalg.norm(ref), 1e-12)
+        worst = max(worst, rel)
+        print(f"bf16 grad {name}: rel {rel:.4f}")
+    assert worst < 0.25, worst  # measured 0.150 (layer-0 weights); a mis-ordered row gives > 1
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3", "bf16"])
+@pytest.mark.parametrize("R,P", [(4, 64), (3, 50), (1024, 64)])
+def test_density_bias_gradient_is_sum(pkg, precision, R, P):
+    """d(sigma)/d(density bias) = 1, so its gradient is exactly sum(g_sigma) whatever the precision of the rest
+    (nerf_mlp.py:173): pins the bias-gradient reduction of the dW kernel in every mode, ragged N included."""
+    from yanerf_amd.pipelines.models import MODELS
+    torch.manual_seed(0)
+    m = MODELS.build(dict(type="NeRFMLP", precision=precision)).to(DEV)
+    o = torch.randn(R, 3, device=DEV) * 0.2 + torch.tensor([0.0, 0.0, 4.0], device=DEV)
+    d = torch.randn(R, 3, device=DEV)
+    z = torch.sort(torch.rand(R, P, device=DEV) * 4 + 2, -1)[0]
+    out = m(o, d, z)
+    gs = torch.randn_like(out["rays_densities"])
+    ((out["rays_densities"] * gs).sum() + out["rays_features"].sum()).backward()
+    exact = gs.double().sum().item()
+    got = m.density_layer.bias.grad.double().item()
+    # bf16 mode stores g_sigma in bf16 (relative rounding 2^-9 per element)
+    tol = 1e-5 if precision != "bf16" else 4e-3 * gs.abs().sum().item() / abs(exact)
+    assert abs(got - exact) <= tol * abs(exact), (got, exact)
+
+
 @pytest.mark.parametrize("precision", FP32_MODES)
 def test_mlp_large_vs_oracle(pkg, precision):
     """65,536 points (1024 rays x 64) of the Lego MLP against the oracle on a 2,048-point subset."""

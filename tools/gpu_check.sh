@@ -5,7 +5,7 @@ set -u
 TAG=${1:-run}; shift || true
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -q -rf -p no:cacheprovider > gpurun_out/gpu_tests_$TAG.log 2>&1
+timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -q -rf -s -p no:cacheprovider > gpurun_out/gpu_tests_$TAG.log 2>&1
 rc=$?; echo "rc=$rc" >> gpurun_out/gpu_tests_$TAG.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py --steps 10 --warmup 3 --no-cpu-baseline "$@" > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?

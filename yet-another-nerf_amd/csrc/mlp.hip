@@ -650,27 +650,69 @@ template <> __device__ __forceinline__ void pk_lds<x3_t>(bf16_t* act, int m, int
   pk_lds<bf16_t>(act + PL, m, n, h1);
   pk_lds<bf16_t>(act + 2 * PL, m, n, h2);
 }
-// store the packed tile into 4 consecutive feature-major rows (stride ld)
-template <typename T> __device__ __forceinline__ void pk_store_rows(typename Cfg<T>::st_t* dst, int64_t ld, Pk<T> p);
-// Plain stores: the scattered 2-/4-byte row segments rely on write-combining in L2 (measured: non-temporal
-// stores made the bf16 forward 2.6x slower).
-template <typename V> __device__ __forceinline__ void st_stream(V* p, V v) { *p = v; }
-template <> __device__ __forceinline__ void pk_store_rows<float>(float* dst, int64_t ld, Pk<float> p) {
-  st_stream(dst, p.v.x);
-  st_stream(dst + ld, p.v.y);
-  st_stream(dst + 2 * ld, p.v.z);
-  st_stream(dst + 3 * ld, p.v.w);
+// Store a packed tile into 4 feature-major rows given the tile's uniform base (layer, row tile, point tile: SGPRs),
+// this lane's byte offset `voff` (4g rows + li points, one VGPR for every tile), the row stride `ldb` and the byte
+// offset `so` of the 16-point group.
+//  bf16: raw buffer stores (voffset = lane, soffset = row / point-group offset): no per-store 64-bit address VALU,
+//        which the 2-byte stores (4 per tile) otherwise pay (measured: bf16 inference forward 0.99 -> 0.90 ms with the
+//        SAVE template);
+//  fp32 / x3: plain global stores (buffer stores measured slower there: fp32 training forward 7.7 -> 8.4 ms).
+// All plain (temporal) stores: the scattered 2-/4-byte row segments rely on write-combining in L2 (measured:
+// non-temporal stores made the bf16 forward 2.6x slower).
+template <typename T>
+__device__ __forceinline__ void pk_store_rows_b(typename Cfg<T>::st_t* base, uint32_t voff, int ldb, int so, Pk<T> p);
+template <>
+__device__ __forceinline__ void pk_store_rows_b<float>(float* base, uint32_t voff, int ldb, int so, Pk<float> p) {
+  char* b = (char*)base + so + voff;
+  *(float*)b = p.v.x;
+  *(float*)(b + ldb) = p.v.y;
+  *(float*)(b + 2 * (int64_t)ldb) = p.v.z;
+  *(float*)(b + 3 * (int64_t)ldb) = p.v.w;
 }
-template <> __device__ __forceinline__ void pk_store_rows<x3_t>(float* dst, int64_t ld, Pk<x3_t> p) {
-  pk_store_rows<float>(dst, ld, Pk<float>{p.v});
+template <>
+__device__ __forceinline__ void pk_store_rows_b<x3_t>(float* base, uint32_t voff, int ldb, int so, Pk<x3_t> p) {
+  pk_store_rows_b<float>(base, voff, ldb, so, Pk<float>{p.v});
 }
-template <> __device__ __forceinline__ void pk_store_rows<bf16_t>(bf16_t* dst, int64_t ld, Pk<bf16_t> p) {
-  st_stream(dst, (bf16_t)p.w0);
-  st_stream(dst + ld, (bf16_t)(p.w0 >> 16));
-  st_stream(dst + 2 * ld, (bf16_t)p.w1);
-  st_stream(dst + 3 * ld, (bf16_t)(p.w1 >> 16));
+template <>
+__device__ __forceinline__ void pk_store_rows_b<bf16_t>(bf16_t* base, uint32_t voff, int ldb, int so, Pk<bf16_t> p) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b16((unsigned short)p.w0, rs, voff, so, 0);
+  __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(p.w0 >> 16), rs, voff, so + ldb, 0);
+  __builtin_amdgcn_raw_buffer_store_b16((unsigned short)p.w1, rs, voff, so + 2 * ldb, 0);
+  __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(p.w1 >> 16), rs, voff, so + 3 * ldb, 0);
+}
+
+// Per-lane trunk ReLU mask word of one layer: 4 bits for each of the lane's NT*MT accumulator tiles.
+//  fp32 / x3: tile t, element r at bit 4t + r (pk_bits);
+//  bf16: tile t, element r at bit 32 (t >> 3) + 8 r + (t & 7): the relu'd halves h in [0, 0x7fff] are nonzero iff
+//        bit 15 of h + 0x7fff is set (both halves of a packed pair in one add, no carry between them), one v_perm
+//        gathers the four flag bytes and a shift + and-or places them.
+template <typename T> __device__ __forceinline__ void mask_acc(uint64_t& bits, Pk<T> h, int t) {
+  bits |= (uint64_t)pk_bits<T>(h) << (4 * t);
+}
+template <> __device__ __forceinline__ void mask_acc<bf16_t>(uint64_t& bits, Pk<bf16_t> h, int t) {
+  const uint32_t f = __builtin_amdgcn_perm(h.w1 + 0x7fff7fffu, h.w0 + 0x7fff7fffu, 0x07050301u);  // flags at 8r + 7
+  const int j = t & 7;
+  const uint32_t w = (f >> (7 - j)) & (0x01010101u << j);
+  bits |= (uint64_t)w << (32 * (t >> 3));
 }
 // zero the elements of v whose bit (bits >> sh .. sh+3) is clear
+__device__ __forceinline__ f4 apply_mask4(f4 v, uint64_t bits, int sh);
+// zero the elements of tile t of a value whose mask bit (mask_acc layout) is clear
+template <typename T> __device__ __forceinline__ f4 apply_mask_tile(f4 v, uint64_t bits, int t) {
+  if constexpr (sizeof(T) == 2 && !is_x3<T>) {
+    const uint32_t w = (uint32_t)(bits >> (32 * (t >> 3)));
+    const int j = t & 7;
+    f4 r;
+    r.x = __int_as_float(__float_as_int(v.x) & __builtin_amdgcn_sbfe(w, j, 1));
+    r.y = __int_as_float(__float_as_int(v.y) & __builtin_amdgcn_sbfe(w, 8 + j, 1));
+    r.z = __int_as_float(__float_as_int(v.z) & __builtin_amdgcn_sbfe(w, 16 + j, 1));
+    r.w = __int_as_float(__float_as_int(v.w) & __builtin_amdgcn_sbfe(w, 24 + j, 1));
+    return r;
+  } else {
+    return apply_mask4(v, bits, 4 * t);
+  }
+}
 __device__ __forceinline__ f4 apply_mask4(f4 v, uint64_t bits, int sh) {
   const uint32_t w = (uint32_t)(bits >> sh);
   f4 r;
@@ -755,7 +797,8 @@ __device__ __forceinline__ void store_mask_tile(uint64_t* masks, int64_t Npad, i
 }
 
 // ============================================================================================ forward
-template <typename T>
+// SAVE: training forward (saved activation rows + ReLU masks for the backward); else inference, outputs only.
+template <typename T, bool SAVE>
 __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_fwd_kernel(
     MlpLayout lay, const typename Cfg<T>::w_t* __restrict__ Wt, const float* __restrict__ Wf,
     const float* __restrict__ origins, const float* __restrict__ dirs, const float* __restrict__ lengths, int64_t R,
@@ -768,11 +811,20 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   static_assert(MT <= WAVES, "one wave per 16-point group in the heads");
   typedef typename Cfg<T>::lds_t LT;
   __shared__ __attribute__((aligned(16))) LT act[Cfg<T>::PLANES * M * ROW];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int64_t N = R * P;
   const int64_t p0 = (int64_t)blockIdx.x * M;
-  const int64_t ld = row_ld(Npad, sizeof(typename Cfg<T>::st_t));
+  typedef typename Cfg<T>::st_t ST;
+  const int64_t ld = row_ld(Npad, sizeof(ST)), ldb = ld * (int64_t)sizeof(ST);
+  const uint32_t soff = (uint32_t)(4 * g * ldb + li * (int64_t)sizeof(ST));  // this lane's offset in a 16x16 row tile
+  if constexpr (!SAVE) saved = nullptr;
+  // bf16 has separate training / inference instantiations (branch-free epilogues); fp32 / x3 keep one kernel that
+  // tests the saved pointer at run time (with a branch-free epilogue the compiler interleaves it into the GEMM loop
+  // and the fp32 MFMA schedule measured slower: training forward 7.7 -> 8.3 ms)
+  constexpr bool STAT = sizeof(T) == 2 && !is_x3<T>;
+  const bool sv = STAT ? SAVE : saved != nullptr;
   const int64_t wpl = lay.t_plane;
   const SavedRows SR = saved_rows(lay.L);
   const int mt_ = tid / TPP, q = tid % TPP;
@@ -790,8 +842,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
 #pragma unroll
   for (int i = 0; i < 3; ++i) x3[i] = o3[i] + t * d3[i];  // models/utils.py:244
   if (!(YANERF_ABLATE & 2))
-    harmonic_to_lds<T>(act, mt_, PE_COL, KPE, x3, lay.fx, lay.ax, q, saved ? saved + SR.pe * ld + p : nullptr,
-                       ld);
+    harmonic_to_lds<T>(act, mt_, PE_COL, KPE, x3, lay.fx, lay.ax, q,
+                       saved ? saved + SR.pe * ld + p : nullptr, ld);
   __syncthreads();
 
   f4 acc[NT][MT];
@@ -819,13 +871,15 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
         const int m = 16 * mt + li;
         if (!(YANERF_ABLATE & 16)) pk_lds<T>(act, m, n, h);
         else if (__float_as_uint(acc[nt][mt].x) == 0x7fc00001u) act[m] = (LT)0;  // keep acc live
-        if (saved && !(YANERF_ABLATE & 4)) {
-          pk_store_rows<T>(saved + (SR.h0 + 256LL * l + n) * ld + p0 + m, ld, h);
-          bits |= (uint64_t)pk_bits<T>(h) << ((nt * MT + mt) * 4);
+        if (sv && !(YANERF_ABLATE & 4)) {
+          pk_store_rows_b<T>((saved + (SR.h0 + 256LL * l + nrow0 + 16 * nt) * ld + p0),
+                               soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
+          mask_acc<T>(bits, h, nt * MT + mt);
         }
       }
     }
-    if (saved && !(YANERF_ABLATE & 4)) masks[(((int64_t)l * gridDim.x + blockIdx.x) * WAVES + wave) * 64 + lane] = bits;
+    if (sv && !(YANERF_ABLATE & 4))
+      masks[(((int64_t)l * gridDim.x + blockIdx.x) * WAVES + wave) * 64 + lane] = bits;
     if (!(YANERF_ABLATE & 32)) __syncthreads();
   }
   // ---- density head: sigma = w_d . h + b_d (nerf_mlp.py:173; density_layer 256->1) as one 16-row MFMA tile per
@@ -853,7 +907,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
         const int m = 16 * mt + li;
         const Pk<T> h = pk_make<T>(v);
         pk_lds<T>(act, m, n, h);
-        if (saved) pk_store_rows<T>(saved + (SR.y + n) * ld + p0 + m, ld, h);
+        if (sv) pk_store_rows_b<T>((saved + (SR.y + nrow0 + 16 * nt) * ld + p0),
+                             soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
       }
     }
   }
@@ -862,8 +917,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     const float nrm = fmaxf(sqrtf(d3[0] * d3[0] + d3[1] * d3[1] + d3[2] * d3[2]), 1e-12f);
     float dn[3] = {d3[0] / nrm, d3[1] / nrm, d3[2] / nrm};
     if (!(YANERF_ABLATE & 2))
-      harmonic_to_lds<T>(act, mt_, PE_COL, KDIR, dn, lay.fd, lay.ad, q, saved ? saved + SR.dpe * ld + p : nullptr,
-                         ld);
+      harmonic_to_lds<T>(act, mt_, PE_COL, KDIR, dn, lay.fd, lay.ad, q,
+                         saved ? saved + SR.dpe * ld + p : nullptr, ld);
   }
   __syncthreads();
   // ---- color layer: LinearWithRepeat(256 + 27 -> 128) + ReLU as one K = 288 GEMM over [Y, dirPE]
@@ -881,8 +936,9 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
         const int m = 16 * mt + li;
         const Pk<T> h = pk_make<T>(v);
         pk_lds<T>(act, m, n, h);
-        if (saved) {
-          pk_store_rows<T>(saved + (SR.c + n) * ld + p0 + m, ld, h);
+        if (sv) {
+          pk_store_rows_b<T>((saved + (SR.c + crow0 + 16 * nt) * ld + p0), soff, (int)ldb,
+                               16 * mt * (int)sizeof(ST), h);
           store_mask_tile(masks + (int64_t)lay.L * trunk_mask_words<T>(Npad), Npad, 0, p0 / 16 + mt,
                           (crow0 + 16 * nt) / 16, v, lane);
         }
@@ -926,7 +982,9 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int64_t p0 = (int64_t)blockIdx.x * M;
-  const int64_t ld = row_ld(Npad, sizeof(typename Cfg<T>::st_t));
+  typedef typename Cfg<T>::st_t ST;
+  const int64_t ld = row_ld(Npad, sizeof(ST)), ldb = ld * (int64_t)sizeof(ST);
+  const uint32_t soff = (uint32_t)(4 * g * ldb + li * (int64_t)sizeof(ST));  // this lane's offset in a row tile
   const int64_t wpl = lay.t_plane;
   const GradRows GR = grad_rows(lay.L);
   const int mt_ = tid / TPP, q = tid % TPP;
@@ -984,7 +1042,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
       f4 v = acc[nt][mt];
       const Pk<T> h = pk_make<T>(v);
       pk_lds<T>(act, m, n, h);
-      pk_store_rows<T>(grad + (GR.dyx + n) * ld + p0 + m, ld, h);
+      pk_store_rows_b<T>((grad + (GR.dyx + nrow0 + 16 * nt) * ld + p0),
+                             soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
     }
   }
   __syncthreads();
@@ -1011,9 +1070,10 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
           v = v + wdv * gsm;
         }
         // ReLU mask of H_{hl}: this lane's own bits of this tile (packed by the forward)
-        const Pk<T> h = pk_make<T>(apply_mask4(v, bits, (nt * MT + mt) * 4));
+        const Pk<T> h = pk_make<T>(apply_mask_tile<T>(v, bits, nt * MT + mt));
         pk_lds<T>(act, m, n, h);
-        pk_store_rows<T>(grad + (GR.dz0 + 256LL * hl + n) * ld + p0 + m, ld, h);
+        pk_store_rows_b<T>((grad + (GR.dz0 + 256LL * hl + nrow0 + 16 * nt) * ld + p0),
+                             soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
       }
     }
     __syncthreads();
@@ -1063,15 +1123,15 @@ template <> constexpr int prec_of<x3_t> = YANERF_PREC_F32X3;
 
 template <typename T> __device__ __forceinline__ float hsum16(f4 v);
 template <> __device__ __forceinline__ float hsum16<float>(f4 v) { return (v.x + v.y) + (v.z + v.w); }
+// bf16: the 8 halves widened exactly (a bf16 is the high half of an fp32) and summed in fp32. (A dot2-with-ones form,
+// __builtin_amdgcn_fdot2_f32_bf16, was miscompiled by this toolchain: the four v_dot2c_f32_bf16 all read the first
+// dword, so every bf16 bias gradient was wrong; caught by tests/test_gpu_parity.py::test_mlp_bf16_gradients_elementwise.)
 template <> __device__ __forceinline__ float hsum16<bf16_t>(f4 v) {
-  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
-  const bf2 one = __builtin_bit_cast(bf2, 0x3f803f80u);
-  float s = 0.f;
-  s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, v.x), one, s, false);
-  s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, v.y), one, s, false);
-  s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, v.z), one, s, false);
-  s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2, v.w), one, s, false);
-  return s;
+  const uint32_t u[4] = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+  float s[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s[i] = __uint_as_float(u[i] << 16) + __uint_as_float(u[i] & 0xffff0000u);
+  return (s[0] + s[1]) + (s[2] + s[3]);
 }
 
 // Stage ring: DW_STAGES buffers of up to 512 rows x 64 B (one K-block of points per row), filled by LDS-DMA
@@ -1559,8 +1619,12 @@ static int launch_fwd(const MlpLayout& L, int prec, const void* packed, const fl
   const float* Wf = (const float*)((const char*)packed + L.f_base);
   dim3 grid((unsigned)(Npad / Cfg<T>::M)), block(Cfg<T>::WAVES * 64);
   uint64_t* masks = saved ? (uint64_t*)((char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST))) : nullptr;
-  hipLaunchKernelGGL(mlp_fwd_kernel<T>, grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, (ST*)saved, masks,
-                     Npad);
+  if (saved || !std::is_same<T, bf16_t>::value)
+    hipLaunchKernelGGL((mlp_fwd_kernel<T, true>), grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, (ST*)saved,
+                       saved ? masks : nullptr, Npad);
+  else
+    hipLaunchKernelGGL((mlp_fwd_kernel<T, false>), grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, nullptr,
+                       nullptr, Npad);
   YN_LAUNCH_CHECK("mlp_forward");
   return 0;
 }

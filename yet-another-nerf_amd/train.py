@@ -116,6 +116,12 @@ class NeRFTrainer:
         self.grad_ptrs = [_C.ptr_array([p.grad.data_ptr() for p in ps]) for ps in self.params]
         self.param_ptrs = [_C.ptr_array([p.data_ptr() for p in ps]) for ps in self.params]
         self.events: Optional[Dict[str, List]] = None  # optional per-phase timing probes
+        # evaluation (full-grid rendering) settings of the same configs (ray_sampler.py:54-56; renderer.py:29-52)
+        self.Pc_eval = int(rs.get("n_pts_per_ray_evaluation", self.Pc))
+        self.Pn_eval = int(rd.get("n_pts_per_ray_fine_evaluation", self.Pn))
+        self.stratified_eval = bool(rs.get("stratified_point_sampling_evaluation", False))
+        self.random_refine_eval = bool(rd.get("stratified_sampling_coarse_evaluation", False))
+        self._eval_ws: Dict[int, Dict[str, torch.Tensor]] = {}
 
     # --------------------------------------------------------------------------------------- timing probes
     def enable_probes(self, names: Sequence[str]):
@@ -139,8 +145,12 @@ class NeRFTrainer:
         return out
 
     # --------------------------------------------------------------------------------------- one step
-    def step(self, pose: torch.Tensor, focal: torch.Tensor, image: torch.Tensor) -> Dict[str, torch.Tensor]:
-        """pose [1,3,4] (or [1,4,4]), focal [1], image [1,H,W,3] resident on the device."""
+    def step(self, pose: torch.Tensor, focal: torch.Tensor, image: torch.Tensor, near: Optional[float] = None,
+             far: Optional[float] = None) -> Dict[str, torch.Tensor]:
+        """pose [1,3,4] (or [1,4,4]), focal [1], image [1,H,W,3] resident on the device; near/far override the
+        configured depth range (LLFF's per-image bounds, averaged as ray_sampler.py:280-283 does)."""
+        near = self.near if near is None else float(near)
+        far = self.far if far is None else float(far)
         L = _C.lib()
         st = ops._stream()
         R = self.R
@@ -154,7 +164,7 @@ class NeRFTrainer:
         # rays: uniform pixel sampling without replacement + stratified depths (Philox)
         seed, off = ops.RNG.next(R * self.Pc)
         _C.check(L.yanerf_raygen(_p(pose), _p(focal), None, None, 1, R, self.W, self.H, float(self.W), float(self.H),
-                                 self.near, self.far, self.Pc, 2 if self.stratified else 0, None, seed, off, _p(self.o),
+                                 near, far, self.Pc, 2 if self.stratified else 0, None, seed, off, _p(self.o),
                                  _p(self.d), _p(self.zc), _p(self.xys), None, st), "yanerf_raygen")
         scale = 1.0 / (R * 3)
         out = {}
@@ -194,6 +204,91 @@ class NeRFTrainer:
                                self.flat.numel, float(self.lr), float(self.betas[0]), float(self.betas[1]),
                                float(self.eps), float(self.weight_decay), self.step_count, st), "yanerf_adam")
         return out
+
+    # --------------------------------------------------------------------------------------- evaluation
+    def _eval_buffers(self, R: int) -> Dict[str, torch.Tensor]:
+        if R not in self._eval_ws:
+            Pf = self.Pc_eval + self.Pn_eval if self.append else self.Pn_eval
+            dev, C = self.dev, self.specs[0].color_dim
+            b = dict(o=torch.empty(R, 3, device=dev), d=torch.empty(R, 3, device=dev),
+                     zc=torch.empty(R, self.Pc_eval, device=dev), zf=torch.empty(R, Pf, device=dev),
+                     xys=torch.empty(R, 2, device=dev), sigma=torch.empty(R * Pf, device=dev),
+                     rgb=torch.empty(R * Pf, C, device=dev), feats=torch.empty(2, R, C, device=dev),
+                     depth=torch.empty(2, R, device=dev), alpha=torch.empty(R, device=dev),
+                     w=torch.empty(R, Pf, device=dev))
+            self._eval_ws = {R: b}  # keep one size
+        return self._eval_ws[R]
+
+    @torch.no_grad()
+    def render(self, pose: torch.Tensor, focal: torch.Tensor, H: Optional[int] = None, W: Optional[int] = None,
+               near: Optional[float] = None, far: Optional[float] = None, chunk: int = 65536):
+        """Full-grid evaluation render of one camera with the current weights, on the fused inference kernels:
+        the reference's EVALUATION pass (nerf_pipeline.py:217-236: FULL_GRID rays, deterministic depths and
+        refinement, no density noise), in chunks of `chunk` rays (it chunks by 131072 points in Python; the result
+        does not depend on the chunking). Returns (rgb [H,W,C] fine, rgb [H,W,C] coarse, depth [H,W] fine)."""
+        L = _C.lib()
+        st = ops._stream()
+        H = int(H or self.H)
+        W = int(W or self.W)
+        near = self.near if near is None else float(near)
+        far = self.far if far is None else float(far)
+        pose = pose.reshape(1, -1, 4)[:, :3, :4].contiguous()
+        focal = focal.reshape(1).contiguous()
+        for i, s in enumerate(self.specs):
+            _C.check(L.yanerf_mlp_pack(ctypes.byref(s.desc()), s.precision, self.param_ptrs[i], _p(self.packed[i]),
+                                       st), "yanerf_mlp_pack")
+        n = H * W
+        R = min(chunk, n)
+        b = self._eval_buffers(R)
+        C = self.specs[0].color_dim
+        out_f = torch.empty(n, C, device=self.dev)
+        out_c = torch.empty(n, C, device=self.dev)
+        out_d = torch.empty(n, device=self.dev)
+        opts = self.march.opts(0, 0.0)
+        for r0 in range(0, n, R):
+            r = min(R, n - r0)
+            ids = torch.arange(r0, r0 + r, device=self.dev, dtype=torch.int64)
+            seed, off = ops.RNG.next(r * self.Pc_eval)
+            _C.check(L.yanerf_raygen(_p(pose), _p(focal), None, _p(ids), 1, r, W, H, float(self.W), float(self.H),
+                                     near, far, self.Pc_eval, 2 if self.stratified_eval else 0, None, seed, off,
+                                     _p(b["o"]), _p(b["d"]), _p(b["zc"]), _p(b["xys"]), None, st), "yanerf_raygen")
+            zs = (b["zc"], b["zf"])
+            for k in range(2):
+                spec = self.specs[k]
+                P = self.Pc_eval if k == 0 else zs[1].shape[1]
+                if k == 1:
+                    seed, off = ops.RNG.next(r * self.Pn_eval)
+                    _C.check(L.yanerf_refine(_p(b["zc"]), _p(b["w"]), r, self.Pc_eval, self.Pn_eval,
+                                             0 if self.random_refine_eval else 1, None, seed, off, int(self.append),
+                                             _p(b["zf"]), st), "yanerf_refine")
+                desc = spec.desc()
+                _C.check(L.yanerf_mlp_forward(ctypes.byref(desc), spec.precision, _p(self.packed[k]), _p(b["o"]),
+                                              _p(b["d"]), _p(zs[k]), r, P, _p(b["sigma"]), _p(b["rgb"]), None, st),
+                         "yanerf_mlp_forward")
+                _C.check(L.yanerf_composite_forward(ctypes.byref(opts), _p(b["sigma"]), _p(b["rgb"]), _p(zs[k]),
+                                                    _p(b["d"]), None, None, r, P, C, _p(b["feats"][k]),
+                                                    _p(b["depth"][k]), _p(b["alpha"]), _p(b["w"]), st),
+                         "yanerf_composite_forward")
+            out_c[r0:r0 + r] = b["feats"][0, :r]
+            out_f[r0:r0 + r] = b["feats"][1, :r]
+            out_d[r0:r0 + r] = b["depth"][1, :r]
+        return out_f.view(H, W, C), out_c.view(H, W, C), out_d.view(H, W)
+
+    def evaluate(self, images) -> Dict[str, float]:
+        """Render every camera of a DeviceImageSet and score it as the reference's eval_one_epoch + create_stats do:
+        per-image MSE of each stage (pipelines/utils.py:137-158), PSNR of the MEAN MSE (runners/utils.py:270-283)."""
+        mse_f, mse_c = [], []
+        for i in range(len(images)):
+            pose, focal, img, nr, fr = images.item(i)
+            near = None if nr is None else float(nr.mean())  # per-image bounds -> scalar (ray_sampler.py:280-283)
+            far = None if fr is None else float(fr.mean())
+            f, c, _ = self.render(pose, focal, images.H, images.W, near, far)
+            mse_f.append(torch.mean((f - img[0]) ** 2))
+            mse_c.append(torch.mean((c - img[0]) ** 2))
+        mf = float(torch.stack(mse_f).mean())
+        mc = float(torch.stack(mse_c).mean())
+        return {"loss_rgb_mse": mf, "loss_prev_stage_rgb_mse": mc, "loss_rgb_psnr": -10.0 * math.log10(max(mf, 1e-12)),
+                "loss_prev_stage_rgb_psnr": -10.0 * math.log10(max(mc, 1e-12))}
 
     # --------------------------------------------------------------------------------------- checkpoints
     def pipeline_state_dict(self) -> Dict[str, torch.Tensor]:

@@ -191,9 +191,11 @@ def linear(x, W, b):
     return y.astype(f32)
 
 
-def nerf_mlp_forward(params: Dict[str, np.ndarray], arch: MLPArch, origins, directions, lengths):
+def nerf_mlp_forward(params: Dict[str, np.ndarray], arch: MLPArch, origins, directions, lengths, code=None):
     """NeRFMLP.forward (nerf_mlp.py:117-177) with MLPWithInputSkips (nerf_mlp.py:267-289) and
     LinearWithRepeat (models/utils.py:207-211). origins/directions (..., 3), lengths (..., P).
+    `code` (latent_dim,): one batch element's global code, appended to every point's xyz embedding
+    (create_embeddings_for_implicit_function / broadcast_global_code, nerf_mlp.py:299-335).
     Returns sigma (..., P, 1), rgb (..., P, C), cache."""
     lead = lengths.shape[:-1]
     P = lengths.shape[-1]
@@ -203,6 +205,8 @@ def nerf_mlp_forward(params: Dict[str, np.ndarray], arch: MLPArch, origins, dire
     t = lengths.reshape(R, P).astype(f32)
     pts = (o[:, None, :] + t[:, :, None] * d[:, None, :]).astype(f32)  # models/utils.py:244
     embed = harmonic_embedding(pts.reshape(R * P, 3), arch.n_harmonic_functions_xyz)
+    if code is not None:
+        embed = np.concatenate([embed, np.broadcast_to(np.asarray(code, f32), (R * P, len(code)))], -1)
     cache = MLPCache(embed=embed, n_rays=R, P=P)
     y = embed
     for li in range(arch.n_layers):

@@ -35,7 +35,8 @@ def param_shapes(arch: dict) -> List[Tuple[str, Tuple[int, ...]]]:
     nl = arch["n_layers"]
     trunk = 256
     hid = arch["n_hidden_neurons_xyz"]
-    xyz_dim = 3 * (2 * arch["n_harmonic_functions_xyz"] + 1)
+    # embeds = [PE(x), global code] (nerf_mlp.py:299-335): latent_dim extra input columns for layer 0 and skips
+    xyz_dim = 3 * (2 * arch["n_harmonic_functions_xyz"] + 1) + arch.get("latent_dim", 0)
     dir_dim = 3 * (2 * arch["n_harmonic_functions_dir"] + 1)
     hdir = arch["n_hidden_neurons_dir"]
     out = []

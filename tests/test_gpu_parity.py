@@ -189,6 +189,41 @@ def test_density_bias_gradient_is_sum(pkg, precision, R, P):
     assert abs(got - exact) <= tol * abs(exact), (got, exact)
 
 
+@pytest.mark.parametrize("precision", FP32_MODES + ["bf16"])
+def test_conditional_mlp_global_codes(pkg, golden, precision):
+    """latent_dim > 0 (reference tests/configs/pipelines/models/nerf_conditional_mlp.yml): each batch element's code
+    is folded into layer 0's and the skip layer's bias; outputs, parameter and code gradients against the reference
+    (golden: make_golden_conditional.py); a code of the wrong width raises ValueError as in the reference."""
+    g = golden("mlp_conditional")
+    arch = dict(LEGO_ARCH, latent_dim=2)
+    m, _ = build_mlp(pkg, arch, int(g["seed"]), precision=precision)
+    codes = t(g["codes"]).requires_grad_(True)
+    out = m(t(g["origins"]), t(g["directions"]), t(g["lengths"]), global_codes=codes)
+    sig, rgb = out["rays_densities"], out["rays_features"]
+    strict = precision != "bf16"
+    close(n(sig), g["sigma"], 2e-5 if strict else 5e-2, 1e-5 if strict else 5e-2)
+    close(n(rgb), g["rgb"], 2e-6 if strict else 2e-2)
+    m.zero_grad()
+    ((sig * t(g["g_sigma"])).sum() + (rgb * t(g["g_rgb"])).sum()).backward()
+    gref = g["g_codes"]
+    if strict:
+        close(n(codes.grad), gref, 1e-5 * max(1.0, np.abs(gref).max()), 1e-4)
+        for name, p in m.named_parameters():
+            v = n(p.grad)
+            if f"grad:{name}" in g:
+                ref = g[f"grad:{name}"]
+                close(v, ref, 1e-5 * max(1.0, np.abs(ref).max()), 1e-4)
+            else:
+                ref = g[f"gradval:{name}"]
+                close(v.reshape(-1)[g[f"gradidx:{name}"]], ref, 1e-5 * max(1.0, np.abs(ref).max()), 1e-4)
+    else:
+        assert np.linalg.norm(n(codes.grad) - gref) <= 0.25 * np.linalg.norm(gref)
+    with pytest.raises(ValueError):
+        m(t(g["origins"]), t(g["directions"]), t(g["lengths"]), global_codes=t(np.zeros((3, 1, 3), np.float32)))
+    with pytest.raises(ValueError):
+        m(t(g["origins"]), t(g["directions"]), t(g["lengths"]))
+
+
 @pytest.mark.parametrize("precision", FP32_MODES)
 def test_mlp_large_vs_oracle(pkg, precision):
     """65,536 points (1024 rays x 64) of the Lego MLP against the oracle on a 2,048-point subset."""
@@ -474,3 +509,36 @@ def test_trainer_checkpoint_interop(pkg, tmp_path):
     tr2.step(poses[2], focal, image)
     torch.cuda.synchronize()
     assert torch.equal(tr2.flat.data, tr.flat.data)
+
+
+def test_pipeline_global_codes(pkg):
+    """The reference's tests/test_pipeline.py:37-64: the conditional-MLP pipeline (latent_dim 2, IdentityMapper feature
+    extractor passing `global_codes` through to both MLPs) in TRAINING mode with a background image; plus a backward
+    pass reaching the codes."""
+    cfg = dict(
+        type="NeRFPipeline",
+        model=dict(type="NeRFMLP", n_layers=8, input_skips=[5], n_harmonic_functions_xyz=10,
+                   harmonic_functions_xyz_append_intput=True, n_hidden_neurons_xyz=256, n_harmonic_functions_dir=4,
+                   harmonic_functions_dir_append_intput=True, n_hidden_neurons_dir=128, latent_dim=2,
+                   input_xyz=True, color_dim=3),
+        ray_sampler=dict(type="RaySampler", image_width=10, image_height=6, n_rays_per_image_sampled_from_mask=4,
+                         min_depth=0.5, max_depth=1.0, scene_extent=0.0, n_pts_per_ray_training=5,
+                         n_pts_per_ray_evaluation=5, stratified_point_sampling_training=True,
+                         stratified_point_sampling_evaluation=False),
+        renderer=dict(type="MultipassEmissionAbsorpsionRenderer", n_pts_per_ray_fine_training=5,
+                      n_pts_per_ray_fine_evaluation=5, append_coarse_samples_to_fine=True,
+                      density_noise_std_train=0.0, bg_color=[0.0, 0.0, 0.0], blend_output=True),
+        chunk_size_grid=30, num_passes=2, loss_weights={"loss_rgb_mse": 1.0, "loss_prev_stage_rgb_mse": 1.0},
+        output_rasterized_mc=True, feature_extractor=dict(type="IdentityMapper"))
+    pipe = pkg["PIPELINES"].build(cfg).to(DEV)
+    torch.manual_seed(0)
+    B = 3
+    poses = torch.randn(B, 3, 4, device=DEV)
+    focal = torch.ones(B, device=DEV) * 500
+    bg = torch.rand(B, 6, 10, 3, device=DEV)
+    codes = torch.randn(B, 2, device=DEV, requires_grad=True)
+    preds = pipe(poses=poses, focal_lengths=focal, bg_image_rgb=bg, image_rgb=torch.rand(B, 6, 10, 3, device=DEV),
+                 evaluation_mode=pkg["EM"].TRAINING, global_codes=codes)
+    assert torch.isfinite(preds["objective"]).all()
+    preds["objective"].mean().backward()
+    assert codes.grad is not None and torch.isfinite(codes.grad).all() and codes.grad.abs().sum() > 0

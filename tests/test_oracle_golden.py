@@ -171,3 +171,18 @@ def test_train_step_lego(golden):
                 idx = g[f"gradidx{i}:{k}"]
                 ref = g[f"gradval{i}:{k}"]
                 close(v.reshape(-1)[idx], ref, 5e-3 * np.abs(ref).max(), 1e-3)
+
+
+def test_conditional_mlp(golden):
+    """Global codes (latent_dim 2, reference tests/configs/pipelines/models/nerf_conditional_mlp.yml): the oracle
+    appends each batch element's code to the xyz embedding; pinned to the reference's outputs."""
+    g = golden("mlp_conditional")
+    arch_d = dict(LEGO_ARCH, latent_dim=2)
+    params = make_nerf_mlp_params(arch_d, int(g["seed"]))
+    np.testing.assert_array_equal(checksum(params), g["checksum"])
+    arch = O.MLPArch.from_dict(arch_d)
+    for b in range(g["origins"].shape[0]):
+        sig, rgb, _ = O.nerf_mlp_forward(params, arch, g["origins"][b], g["directions"][b], g["lengths"][b],
+                                         code=g["codes"][b].reshape(-1))
+        np.testing.assert_allclose(sig, g["sigma"][b], atol=2e-5, rtol=1e-5)
+        np.testing.assert_allclose(rgb, g["rgb"][b], atol=2e-6)

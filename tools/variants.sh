@@ -8,6 +8,6 @@ mkdir -p gpurun_out
 for V in "$@"; do
   NAME=${V%%=*}; FLAGS=${V#*=}
   make -s -C yet-another-nerf_amd/csrc OUT=/tmp/libyanerf_$NAME.so EXTRA="$FLAGS" > /dev/null || exit 1
-  YANERF_HIP_LIB=/tmp/libyanerf_$NAME.so timeout -k 10 200 python tools/microbench.py > gpurun_out/${TAG}_$NAME.json 2>gpurun_out/${TAG}_$NAME.err || exit $?
+  YANERF_HIP_LIB=/tmp/libyanerf_$NAME.so timeout -k 10 200 python tools/microbench.py ${PREC:-} > gpurun_out/${TAG}_$NAME.json 2>gpurun_out/${TAG}_$NAME.err || exit $?
   echo "$NAME $(cat gpurun_out/${TAG}_$NAME.json)"
 done

@@ -119,10 +119,10 @@ class NeRFMLP(torch.nn.Module):
 
     # ------------------------------------------------------------------ HIP path
     def spec(self) -> ops.MlpSpec:
-        if self.latent_dim != 0 or not self.input_xyz or not self.input_dir or self.nerf_paper_v1:
+        if not self.input_xyz or not self.input_dir or self.nerf_paper_v1:
             raise NotImplementedError(
-                "the HIP NeRFMLP covers latent_dim=0, input_xyz=True, input_dir=True, nerf_paper_v1=False "
-                "(the Lego/Fern configurations)")
+                "the HIP NeRFMLP covers input_xyz=True, input_dir=True, nerf_paper_v1=False (every reference "
+                "configuration; latent codes are supported)")
         return ops.MlpSpec(n_layers=self.n_layers, input_skips=tuple(self.input_skips),
                            n_harmonic_functions_xyz=self.n_harmonic_functions_xyz,
                            n_harmonic_functions_dir=self.n_harmonic_functions_dir,
@@ -152,10 +152,44 @@ class NeRFMLP(torch.nn.Module):
             self._pack_key = key
         return self._packed
 
+    def _check_input(self, global_codes) -> bool:  # nerf_mlp.py:179-183
+        if global_codes is None:
+            return self.latent_dim == 0
+        return global_codes.shape[-1] == self.latent_dim
+
+    def _coded_params(self, code: torch.Tensor) -> List[torch.Tensor]:
+        """Parameters with a global code folded in. The code is appended to the xyz embedding (embeds = [PE(x),
+        code], nerf_mlp.py:299-335) and therefore enters layer 0 and every skip layer ([h, PE(x), code],
+        nerf_mlp.py:280-283) through their last latent_dim weight columns; being constant over the batch element's
+        points, W[:, code cols] @ code is a bias. The kernel runs with the PE columns only and bias' = b + W_c code;
+        autograd carries the bias gradient back to W_c and to the code."""
+        ps = []
+        for li, layer in enumerate(self.xyz_encoder.mlp):
+            w, b = layer[0].weight, layer[0].bias
+            if li == 0 or li in self.xyz_encoder._input_skips:
+                keep = w.shape[1] - self.latent_dim  # pe (layer 0) or hidden + pe (skip layers)
+                b = b + w[:, keep:] @ code
+                w = w[:, :keep].contiguous()
+            ps += [w, b]
+        return ps + self.hip_params()[2 * len(self.xyz_encoder.mlp):]
+
     def forward(self, origins: torch.Tensor, directions: torch.Tensor, lengths: torch.Tensor,
                 global_codes: Optional[torch.Tensor] = None, **kwargs) -> dict:
+        """nerf_mlp.py:117-177. global_codes [B, N_latents, latent_dim] (flattened per batch element, :160-161)."""
         if global_codes is not None:
-            raise NotImplementedError("global_codes (latent_dim > 0) are not on the HIP path")
+            global_codes = global_codes.view(global_codes.shape[0], -1)
+        if not self._check_input(global_codes):
+            raise ValueError("The shape of global codes is imcompible with the input dim of the network.")
         spec = self.spec()
-        sigma, rgb = ops.mlp_forward(spec, self.packed_weights(spec), origins, directions, lengths, self.hip_params())
+        if global_codes is None:
+            sigma, rgb = ops.mlp_forward(spec, self.packed_weights(spec), origins, directions, lengths,
+                                         self.hip_params())
+            return dict(rays_densities=sigma, rays_features=rgb, aux={})
+        outs = []
+        for b in range(origins.shape[0]):  # one launch per batch element: its code is a per-layer bias
+            ps = self._coded_params(global_codes[b].to(origins.dtype))
+            outs.append(ops.mlp_forward(spec, ops.mlp_pack(spec, ps), origins[b:b + 1], directions[b:b + 1],
+                                        lengths[b:b + 1], ps))
+        sigma = torch.cat([o[0] for o in outs], 0)
+        rgb = torch.cat([o[1] for o in outs], 0)
         return dict(rays_densities=sigma, rays_features=rgb, aux={})

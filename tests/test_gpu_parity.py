@@ -542,3 +542,33 @@ def test_pipeline_global_codes(pkg):
     assert torch.isfinite(preds["objective"]).all()
     preds["objective"].mean().backward()
     assert codes.grad is not None and torch.isfinite(codes.grad).all() and codes.grad.abs().sum() > 0
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_fused_render_matches_registry_pipeline(pkg, precision):
+    """NeRFTrainer.render (fused evaluation path: few large chunks, no autograd) against the registry NeRFPipeline's
+    EVALUATION forward with the same weights: same kernels and deterministic depths/refinement, so the images agree
+    to float round-off (the pipeline's chunking is result-invariant, test_chunking_invariance)."""
+    import yanerf_boot  # noqa: F401
+    from yanerf_amd.train import NeRFTrainer
+    from yanerf_amd.utils.config import Config
+    from scene import synthetic_pose
+    cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml")).pipeline
+    cfg.model.precision = precision
+    tr = NeRFTrainer(cfg, precision=precision, device=DEV, n_rays=256, seed=4)
+    pipe = pkg["PIPELINES"].build(cfg).to(DEV)
+    pipe.load_state_dict(tr.pipeline_state_dict(), strict=False)
+    pipe.eval()
+    pose = torch.from_numpy(synthetic_pose(20.0, -30.0, 4.0)).float()[None, :3, :4].contiguous().to(DEV)
+    focal = torch.tensor([1111.111], device=DEV)
+    H, W = 16, 24
+    with torch.no_grad():
+        ref = pipe(poses=pose, focal_lengths=focal, image_height=H, image_width=W,
+                   evaluation_mode=pkg["EM"].EVALUATION)
+        rb = pipe.ray_sampler(pose, focal, evaluation_mode=pkg["EM"].EVALUATION, image_height=H, image_width=W)
+        ro = pipe.renderer(*rb, bg_color=None, implicit_functions=pipe.implicit_functions,
+                           evaluation_mode=pkg["EM"].EVALUATION)
+    f, c, d = tr.render(pose, focal, H, W, chunk=100)  # ragged chunks on purpose
+    np.testing.assert_allclose(n(f), n(ref["rendered_images"]).reshape(H, W, 3), atol=1e-6, rtol=0)
+    np.testing.assert_allclose(n(c), n(ro.prev_stage.features).reshape(H, W, 3), atol=1e-6, rtol=0)
+    np.testing.assert_allclose(n(d), n(ro.depths).reshape(H, W), atol=1e-5, rtol=0)

@@ -98,3 +98,24 @@ def test_device_image_set_and_sampler_order(dirs):
                 assert list(dev.epoch_order(epoch, rank, world, shuffle=False, drop_last=False)) == list(ref)
     ll = DeviceImageSet(LLFFDataset(str(dirs / "fern"), "train", test_skip=4, factor=8), "cpu")
     assert ll.near is not None and ll.near.shape == (len(ll),) and torch.all(ll.far > ll.near)
+
+
+@pytest.mark.parametrize("name,sub,splits", [("lego", "lego", ("train", "test")), ("fern", "fern", ("train", "test"))])
+def test_product_config_datasets_build(dirs, name, sub, splits):
+    """The `datasets:` entries of the product configs (lego.yml / fern.yml) build through DATASETS as in run.py:95-110
+    (base_dir pointed at the synthetic fixture; fern.yml's defaults factor=8 / test_skip=8 apply)."""
+    import copy
+
+    import yanerf_boot
+    from yanerf_amd.datasets import DATASETS
+    from yanerf_amd.utils.config import Config
+    cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / f"configs/nerf/{name}.yml"))
+    for entry in cfg.datasets:
+        if entry["split"] not in splits:
+            continue
+        e = copy.deepcopy(dict(entry))
+        e["base_dir"] = str(dirs / sub)
+        ds = DATASETS.build(e)
+        assert len(ds) > 0
+        item = ds[0]
+        assert item[0].shape[-1] == 4 and item[2].shape[-1] == 3

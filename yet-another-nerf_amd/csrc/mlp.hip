@@ -28,6 +28,16 @@
 #ifndef YANERF_ABLATE
 #define YANERF_ABLATE 0
 #endif
+// bf16 forward wave tile: 4 waves x (64 features x 128 points) -- half the LDS operand reads per MFMA of the 8-wave
+// (32 x 128) tiling, twice the accumulators; measured training forward 1.47 -> 1.26 ms, inference 0.92 -> 0.77 ms.
+// The dX kernel keeps 8 waves (its colour-head VALU work and 2-byte row stores want the wave count: 3.2 -> 3.8 ms
+// with 4). The ReLU-mask words the forward writes land in the dX kernel's layout either way (mask_w).
+#ifndef YANERF_BF16_WAVES
+#define YANERF_BF16_WAVES 4
+#endif
+#ifndef YANERF_BF16_DXWAVES
+#define YANERF_BF16_DXWAVES 8
+#endif
 #ifndef YANERF_LOWREG
 #define YANERF_LOWREG 0
 #endif
@@ -45,20 +55,25 @@ struct x3_t {};
 // of the saved activations / gradients in HBM and of the packed weights
 template <typename T> struct Cfg;
 template <> struct Cfg<float> {
-  static constexpr int M = 64, WAVES = 4, EPC = 4, KB = 16, APREF = 1, LOWREG = 0, WPE = 2, PLANES = 1;
+  static constexpr int M = 64, WAVES = 4, DXWAVES = 4, EPC = 4, KB = 16, APREF = 1, LOWREG = 0, WPE = 2, PLANES = 1;
   typedef float lds_t;
   typedef float st_t;
   typedef float w_t;
 };
 template <> struct Cfg<bf16_t> {
-  static constexpr int M = 128, WAVES = 8, EPC = 8, KB = 32, APREF = 3, LOWREG = YANERF_LOWREG, WPE = LOWREG ? 4 : 2;
+  static constexpr int M = 128, WAVES = YANERF_BF16_WAVES, DXWAVES = YANERF_BF16_DXWAVES, EPC = 8, KB = 32,
+                       APREF = YANERF_BF16_WAVES == 4 ? 2 : 3, LOWREG = YANERF_LOWREG, WPE = LOWREG ? 4 : 2;
   static constexpr int PLANES = 1;
   typedef bf16_t lds_t;
   typedef bf16_t st_t;
   typedef bf16_t w_t;
 };
+#ifndef YANERF_X3_APREF
+#define YANERF_X3_APREF 2
+#endif
 template <> struct Cfg<x3_t> {
-  static constexpr int M = 64, WAVES = 8, EPC = 8, KB = 32, APREF = 2, LOWREG = 0, WPE = 2, PLANES = 3;
+  static constexpr int M = 64, WAVES = 8, DXWAVES = 8, EPC = 8, KB = 32, APREF = YANERF_X3_APREF, LOWREG = 0, WPE = 2,
+                       PLANES = 3;
   typedef bf16_t lds_t;
   typedef float st_t;
   typedef bf16_t w_t;
@@ -130,9 +145,13 @@ __host__ __device__ inline GradRows grad_rows(int L) {
 //    point lane&15), read per point by the VALU colour-head backward.
 // Both are 256 bits per point per layer (trunk: 512 in x3, whose 8-wave tiles hold 64 points).
 __host__ __device__ inline int64_t mask_words_per_slot(int64_t Npad) { return Npad / 16 * 16 * 4; }
-// u64 words of one trunk layer's per-lane masks: one per lane of every wave of every point tile
+// u64 mask words per lane per trunk layer: 4 bits for each of the lane's NT x MT accumulator tiles, 16 tiles a word
+template <typename T> __host__ __device__ constexpr int mask_w() {
+  return ((256 / 16 / Cfg<T>::WAVES) * (Cfg<T>::M / 16) + 15) / 16;
+}
+// u64 words of one trunk layer's per-lane masks, indexed ((wg * WAVES + wave) * MW + w) * 64 + lane
 template <typename T> __host__ __device__ inline int64_t trunk_mask_words(int64_t Npad) {
-  return Npad / Cfg<T>::M * Cfg<T>::WAVES * 64;
+  return Npad / Cfg<T>::M * Cfg<T>::WAVES * 64 * mask_w<T>();
 }
 static int64_t trunk_mask_words_prec(int prec, int64_t Npad) {
   return prec == YANERF_PREC_F32    ? trunk_mask_words<float>(Npad)
@@ -507,6 +526,49 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
     if (kb < nkb) step(kb, a[0], false);
     return;
   }
+  if constexpr (sizeof(T) == 2 && MT == 8 && NT >= 4) {
+    // bf16 with 64-feature x 128-point wave tiles: 128 accumulator VGPRs leave room for one K-block of LDS fragments
+    // only, so the K-block is split into two 4-tile point halves and each half's fragments are read while the other
+    // half multiplies (two 16-VGPR half buffers instead of a 64-VGPR double buffer)
+    constexpr int D = Cfg<T>::APREF, MH = MT / 2;
+    f4(&a)[D][1][NT] = R.a;
+    f4 b0[MH], b1[MH];
+#pragma unroll
+    for (int mt = 0; mt < MH; ++mt) b0[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + g);
+    auto step = [&](int kb, f4(&ar)[NT], bool refill) {
+      const int kn = kb + 1 < nkb ? kb + 1 : kb;
+#pragma unroll
+      for (int mt = 0; mt < MH; ++mt) b1[mt] = lds_chunk<T>(act, 16 * (mt + MH) + li, kc0 + kb * 4 + g);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < MH; ++mt) acc[nt][mt] = mma_blk<T>(ar[nt], b0[mt], acc[nt][mt]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int mt = 0; mt < MH; ++mt) b0[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + kn * 4 + g);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < MH; ++mt) acc[nt][mt + MH] = mma_blk<T>(ar[nt], b1[mt], acc[nt][mt + MH]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (refill) {
+        const int ka = kb + D < nkb ? kb + D : nkb - 1;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) ar[nt] = *(const f4*)(wp[nt] + ka * FRAG);
+      }
+    };
+    int kb = 0;
+    for (; kb + D <= nkb; kb += D) {
+#pragma unroll
+      for (int r = 0; r < D; ++r) step(kb + r, a[r][0], true);
+    }
+#pragma unroll
+    for (int r = 0; r < D - 1; ++r)
+      if (kb + r < nkb) step(kb + r, a[r][0], false);
+    return;
+  }
   if constexpr (sizeof(T) == 2) {
     constexpr int D = Cfg<T>::APREF;
     f4(&a)[D][1][NT] = R.a;
@@ -682,26 +744,27 @@ __device__ __forceinline__ void pk_store_rows_b<bf16_t>(bf16_t* base, uint32_t v
   __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(p.w1 >> 16), rs, voff, so + 3 * ldb, 0);
 }
 
-// Per-lane trunk ReLU mask word of one layer: 4 bits for each of the lane's NT*MT accumulator tiles.
-//  fp32 / x3: tile t, element r at bit 4t + r (pk_bits);
-//  bf16: tile t, element r at bit 32 (t >> 3) + 8 r + (t & 7): the relu'd halves h in [0, 0x7fff] are nonzero iff
+// Per-lane trunk ReLU mask words of one layer: 4 bits for each of the lane's NT*MT accumulator tiles, tile t in
+// word t >> 4; within the word (u = t & 15):
+//  fp32 / x3: element r at bit 4u + r (pk_bits);
+//  bf16: element r at bit 32 (u >> 3) + 8 r + (u & 7): the relu'd halves h in [0, 0x7fff] are nonzero iff
 //        bit 15 of h + 0x7fff is set (both halves of a packed pair in one add, no carry between them), one v_perm
 //        gathers the four flag bytes and a shift + and-or places them.
-template <typename T> __device__ __forceinline__ void mask_acc(uint64_t& bits, Pk<T> h, int t) {
-  bits |= (uint64_t)pk_bits<T>(h) << (4 * t);
+// (Called without explicit template arguments so the bf16 overload is picked by partial ordering.)
+template <typename T, int W> __device__ __forceinline__ void mask_acc(uint64_t (&bits)[W], Pk<T> h, int t) {
+  bits[t >> 4] |= (uint64_t)pk_bits<T>(h) << (4 * (t & 15));
 }
-template <> __device__ __forceinline__ void mask_acc<bf16_t>(uint64_t& bits, Pk<bf16_t> h, int t) {
+template <int W> __device__ __forceinline__ void mask_acc(uint64_t (&bits)[W], Pk<bf16_t> h, int t) {
   const uint32_t f = __builtin_amdgcn_perm(h.w1 + 0x7fff7fffu, h.w0 + 0x7fff7fffu, 0x07050301u);  // flags at 8r + 7
   const int j = t & 7;
   const uint32_t w = (f >> (7 - j)) & (0x01010101u << j);
-  bits |= (uint64_t)w << (32 * (t >> 3));
+  bits[t >> 4] |= (uint64_t)w << (32 * ((t >> 3) & 1));
 }
-// zero the elements of v whose bit (bits >> sh .. sh+3) is clear
 __device__ __forceinline__ f4 apply_mask4(f4 v, uint64_t bits, int sh);
 // zero the elements of tile t of a value whose mask bit (mask_acc layout) is clear
-template <typename T> __device__ __forceinline__ f4 apply_mask_tile(f4 v, uint64_t bits, int t) {
+template <typename T, int W> __device__ __forceinline__ f4 apply_mask_tile(f4 v, const uint64_t (&bits)[W], int t) {
   if constexpr (sizeof(T) == 2 && !is_x3<T>) {
-    const uint32_t w = (uint32_t)(bits >> (32 * (t >> 3)));
+    const uint32_t w = (uint32_t)(bits[t >> 4] >> (32 * ((t >> 3) & 1)));
     const int j = t & 7;
     f4 r;
     r.x = __int_as_float(__float_as_int(v.x) & __builtin_amdgcn_sbfe(w, j, 1));
@@ -710,7 +773,7 @@ template <typename T> __device__ __forceinline__ f4 apply_mask_tile(f4 v, uint64
     r.w = __int_as_float(__float_as_int(v.w) & __builtin_amdgcn_sbfe(w, 24 + j, 1));
     return r;
   } else {
-    return apply_mask4(v, bits, 4 * t);
+    return apply_mask4(v, bits[t >> 4], 4 * (t & 15));
   }
 }
 __device__ __forceinline__ f4 apply_mask4(f4 v, uint64_t bits, int sh) {
@@ -733,17 +796,18 @@ __device__ __forceinline__ void harmonic_to_lds(typename Cfg<T>::lds_t* act, int
                                                 typename Cfg<T>::st_t* sv, int64_t ld) {
   constexpr int TPP = Cfg<T>::WAVES * 64 / Cfg<T>::M;
   if constexpr (!is_x3<T> && sizeof(T) == 2) {
-    // bf16 mode: thread q < 3 takes coordinate q at every frequency with the hardware sin/cos of the angle
-    // reduced to revolutions (|error| ~1e-4 rad at the top frequency, far below the bf16 rounding of the value);
-    // thread 3 writes [x, zero padding]
-    static_assert(TPP == 4, "bf16 harmonic split");
-    if (q < 3) {
-      const float xi = q == 0 ? x[0] : (q == 1 ? x[1] : x[2]);
+    // bf16 mode: the hardware sin/cos of the angle reduced to revolutions (|error| ~1e-4 rad at the top frequency,
+    // far below the bf16 rounding of the value). TPP == 4: thread q < 3 takes coordinate q at every frequency,
+    // thread 3 writes [x, zero padding]; TPP == 2: thread 0 takes coordinates 0 and 2, thread 1 coordinate 1 and
+    // [x, padding].
+    static_assert(TPP == 4 || TPP == 2, "bf16 harmonic split");
+    auto coord = [&](int c) {
+      const float xi = c == 0 ? x[0] : (c == 1 ? x[1] : x[2]);
       const float r0 = xi * 0.15915494309189535f;
       for (int f = 0; f < F; ++f) {
         const float r = __builtin_amdgcn_fractf(r0 * (float)(1 << f));
         const float sn = __builtin_amdgcn_sinf(r), cs = __builtin_amdgcn_cosf(r);
-        const int j = q * F + f;
+        const int j = c * F + f;
         lds_put1<T>(act, m, col0 + j, sn);
         lds_put1<T>(act, m, col0 + 3 * F + j, cs);
         if (sv) {
@@ -751,7 +815,8 @@ __device__ __forceinline__ void harmonic_to_lds(typename Cfg<T>::lds_t* act, int
           sv[(int64_t)(3 * F + j) * ld] = to_st<T>(cs);
         }
       }
-    } else {
+    };
+    auto tail = [&]() {
       for (int k = 6 * F; k < width; ++k) {
         const int a = k - 6 * F;
         float v = a == 0 ? x[0] : 0.0f;
@@ -761,6 +826,14 @@ __device__ __forceinline__ void harmonic_to_lds(typename Cfg<T>::lds_t* act, int
         lds_put1<T>(act, m, col0 + k, v);
         if (sv) sv[(int64_t)k * ld] = to_st<T>(v);
       }
+    };
+    if constexpr (TPP == 4) {
+      if (q < 3) coord(q);
+      else tail();
+    } else {
+      coord(q);
+      if (q == 0) coord(2);
+      else tail();
     }
     return;
   }
@@ -807,8 +880,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   constexpr int M = Cfg<T>::M, WAVES = Cfg<T>::WAVES, MT = M / 16;
   constexpr int NT = 256 / 16 / WAVES, NTC = HC / 16 / WAVES;
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB, TPP = WAVES * 64 / M;  // threads per point
-  static_assert(NT * MT <= 16, "per-lane mask word holds at most 16 tiles x 4 bits");
-  static_assert(MT <= WAVES, "one wave per 16-point group in the heads");
+  constexpr int MW = mask_w<T>();  // u64 ReLU-mask words per lane per layer
   typedef typename Cfg<T>::lds_t LT;
   __shared__ __attribute__((aligned(16))) LT act[Cfg<T>::PLANES * M * ROW];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -861,7 +933,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
       ring_fill<T, NT>(ring, Wt + lay.w_off[l + 1], wpl, lay.kpad[l + 1], nrow0, lay.kpad[l + 1] / KB, lane);
     else ring_fill<T, NT>(ring, Wt + lay.wint_off, wpl, 256, nrow0, 256 / KB, lane);
     if (!(YANERF_ABLATE & 32)) __syncthreads();
-    uint64_t bits = 0;
+    uint64_t bits[MW] = {};
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int n = nrow0 + 16 * nt + 4 * g;
@@ -874,22 +946,30 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
         if (sv && !(YANERF_ABLATE & 4)) {
           pk_store_rows_b<T>((saved + (SR.h0 + 256LL * l + nrow0 + 16 * nt) * ld + p0),
                                soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
-          mask_acc<T>(bits, h, nt * MT + mt);
+          mask_acc(bits, h, nt * MT + mt);
         }
       }
     }
     if (sv && !(YANERF_ABLATE & 4))
-      masks[(((int64_t)l * gridDim.x + blockIdx.x) * WAVES + wave) * 64 + lane] = bits;
+#pragma unroll
+      for (int w = 0; w < MW; ++w)
+        masks[((((int64_t)l * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane] = bits[w];
     if (!(YANERF_ABLATE & 32)) __syncthreads();
   }
   // ---- density head: sigma = w_d . h + b_d (nerf_mlp.py:173; density_layer 256->1) as one 16-row MFMA tile per
-  // wave over its 16 points (rows past 0 are zero weights); lanes g == 0 hold sigma of point 16 * wave + li.
-  // Shifting the LDS base by 16 * wave rows keeps the row swizzle (it depends on the row mod 16).
-  float sig = 0.f;
-  if (!(YANERF_ABLATE & 8) && wave < MT) {
-    f4 hacc[1][1];
-    gemm_lds<T, 1, 1>(Wt + lay.wdh_off, wpl, 256, 0, act + 16 * wave * ROW, 0, 256 / KB, hacc, lane);
-    sig = hacc[0][0].x + Wf[lay.bd_off];
+  // 16-point group (rows past 0 are zero weights); wave w takes groups w, w + WAVES, ...; lanes g == 0 hold sigma of
+  // point 16 * group + li. Shifting the LDS base by 16 * group rows keeps the row swizzle (it depends on row mod 16).
+  constexpr int HG = (MT + WAVES - 1) / WAVES;  // head groups per wave
+  float sig[HG];
+#pragma unroll
+  for (int hg = 0; hg < HG; ++hg) {
+    const int grp = wave + hg * WAVES;
+    sig[hg] = 0.f;
+    if (!(YANERF_ABLATE & 8) && grp < MT) {
+      f4 hacc[1][1];
+      gemm_lds<T, 1, 1>(Wt + lay.wdh_off, wpl, 256, 0, act + 16 * grp * ROW, 0, 256 / KB, hacc, lane);
+      sig[hg] = hacc[0][0].x + Wf[lay.bd_off];
+    }
   }
   // ---- intermediate_linear (no activation)
   gemm_lds<T, NT, MT>(Wt + lay.wint_off, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, Wf + lay.bint_off, &ring);
@@ -947,13 +1027,15 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   }
   __syncthreads();
   // ---- output layer 128 -> color_dim + sigmoid, as for the density head (nerf_mlp.py:169-171)
-  {
+#pragma unroll
+  for (int hg = 0; hg < HG; ++hg) {
+    const int grp = wave + hg * WAVES;
     f4 hacc[1][1] = {{f4{0.f, 0.f, 0.f, 0.f}}};
-    if (!(YANERF_ABLATE & 8) && wave < MT)
-      gemm_lds<T, 1, 1>(Wt + lay.woh_off, wpl, HC, 0, act + 16 * wave * ROW, 0, HC / KB, hacc, lane);
-    const int64_t pw = p0 + 16 * wave + li;
-    if (wave < MT && g == 0 && pw < N) {
-      sigma[pw] = sig;
+    if (!(YANERF_ABLATE & 8) && grp < MT)
+      gemm_lds<T, 1, 1>(Wt + lay.woh_off, wpl, HC, 0, act + 16 * grp * ROW, 0, HC / KB, hacc, lane);
+    const int64_t pw = p0 + 16 * grp + li;
+    if (grp < MT && g == 0 && pw < N) {
+      sigma[pw] = sig[hg];
       const float u[CMAX] = {hacc[0][0].x, hacc[0][0].y, hacc[0][0].z, hacc[0][0].w};
 #pragma unroll
       for (int j = 0; j < CMAX; ++j) {
@@ -968,12 +1050,18 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
 
 // ============================================================================================ backward dX
 template <typename T>
-__global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_bwd_dx_kernel(
+__global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_bwd_dx_kernel(
     MlpLayout lay, const typename Cfg<T>::w_t* __restrict__ Wt, const float* __restrict__ Wf,
     const uint64_t* __restrict__ masks, const float* __restrict__ rgb, const float* __restrict__ g_sigma,
     const float* __restrict__ g_rgb, int64_t N, int64_t Npad, typename Cfg<T>::st_t* __restrict__ grad) {
-  constexpr int M = Cfg<T>::M, WAVES = Cfg<T>::WAVES, MT = M / 16;
-  constexpr int NT = 256 / 16 / WAVES;
+  constexpr int M = Cfg<T>::M, WAVES = Cfg<T>::DXWAVES, MT = M / 16;
+  // ReLU-mask words: the forward (Cfg::WAVES waves) wrote mask_w<T>() words per lane per layer; a dX wave whose
+  // NT x MT tiles are exactly one 16-tile word of a forward wave reads that word at the same index
+  // ((layer * grid + wg) * DXWAVES + wave) * 64 + lane, with the same bit positions
+  constexpr int NT = 256 / 16 / WAVES, MW = (NT * MT + 15) / 16;
+  static_assert(Cfg<T>::WAVES * mask_w<T>() == WAVES * MW &&
+                    (Cfg<T>::WAVES == WAVES || (NT * MT == 16 && (256 / 16 / Cfg<T>::WAVES) % NT == 0)),
+                "dX wave tiles must map onto the forward's mask words");
   constexpr int KB = Cfg<T>::KB, TPP = WAVES * 64 / M, CPT = HC / TPP;  // colour columns per thread
   static_assert(CPT % 16 == 0, "colour-head backward: whole 16-feature tiles per thread");
   typedef typename Cfg<T>::lds_t LT;
@@ -1052,7 +1140,10 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     // l == L: the heads -> last trunk layer; else trunk layer l -> layer l-1
     const typename Cfg<T>::w_t* A = (l == lay.L) ? Wt + lay.wintT_off : Wt + lay.wt_off[l];
     const int hl = l - 1;  // layer whose output gradient we form
-    const uint64_t bits = masks[(((int64_t)hl * gridDim.x + blockIdx.x) * WAVES + wave) * 64 + lane];
+    uint64_t bits[MW];
+#pragma unroll
+    for (int w = 0; w < MW; ++w)
+      bits[w] = masks[((((int64_t)hl * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane];
     gemm_lds<T, NT, MT>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring);
     if (l - 1 >= 1) ring_fill<T, NT>(ring, Wt + lay.wt_off[l - 1], wpl, 256, nrow0, 256 / KB, lane);
     __syncthreads();
@@ -1070,7 +1161,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
           v = v + wdv * gsm;
         }
         // ReLU mask of H_{hl}: this lane's own bits of this tile (packed by the forward)
-        const Pk<T> h = pk_make<T>(apply_mask_tile<T>(v, bits, nt * MT + mt));
+        const Pk<T> h = pk_make<T>(apply_mask_tile<T, MW>(v, bits, nt * MT + mt));
         pk_lds<T>(act, m, n, h);
         pk_store_rows_b<T>((grad + (GR.dz0 + 256LL * hl + nrow0 + 16 * nt) * ld + p0),
                              soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
@@ -1641,7 +1732,7 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   int64_t grad_bytes = GR.rows * row_ld(Npad, sizeof(ST)) * (int64_t)sizeof(ST);
   float* slab = (float*)((char*)ws + grad_bytes);
   const uint64_t* masks = (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST)));
-  hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::WAVES * 64), 0, st, L, Wt,
+  hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::DXWAVES * 64), 0, st, L, Wt,
                      Wf, masks, rgb, gs, gr, N, Npad, gradbuf);
   YN_LAUNCH_CHECK("mlp_backward_dx");
   DwJobs D;

@@ -1102,16 +1102,21 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         cw[t][r] = masks[lay.L * trunk_mask_words<T>(Npad) + mask_index(Npad, 0, p / 16, TT * q + t) + r];
-    for (int c = CPT * q; c < CPT * q + CPT; ++c) {
-      float dc = 0.0f;
-      for (int j = 0; j < cd; ++j) dc += du[j] * wo[j * HC + c];
-      const int cl = c & 15;  // feature within its 16-feature tile: ballot word cl & 3, bit 16 * (cl >> 2) + point
-      const uint64_t word = cw[(c - CPT * q) >> 4][cl & 3];
-      const bool on = (word >> (16 * (cl >> 2) + (mt_ & 15))) & 1ull;
-      float dz = on ? dc : 0.0f;
-      lds_put1<T>(act, mt_, c, dz);
-      grad[(GR.dzc + c) * ld + p] = to_st<T>(dz);
-    }
+    // statically indexed (tile t, feature cl) loops keep the mask words in registers (a runtime index into cw
+    // would put it in scratch)
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+      for (int cl = 0; cl < 16; ++cl) {
+        const int c = CPT * q + 16 * t + cl;
+        float dc = 0.0f;
+        for (int j = 0; j < cd; ++j) dc += du[j] * wo[j * HC + c];
+        // feature cl within its 16-feature tile: ballot word cl & 3, bit 16 * (cl >> 2) + point
+        const bool on = (cw[t][cl & 3] >> (16 * (cl >> 2) + (mt_ & 15))) & 1ull;
+        float dz = on ? dc : 0.0f;
+        lds_put1<T>(act, mt_, c, dz);
+        grad[(GR.dzc + c) * ld + p] = to_st<T>(dz);
+      }
   }
   __syncthreads();
   f4 acc[NT][MT];

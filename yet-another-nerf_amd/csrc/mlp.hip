@@ -24,7 +24,8 @@
 #include "common.hpp"
 
 // Development-only timing ablations (never set in the product build): 1 = no MFMA, 2 = no harmonic embedding,
-// 4 = no saved stores in the trunk epilogue, 8 = no VALU heads, 16 = no trunk LDS writes, 32 = no trunk barriers.
+// 4 = no saved stores in the trunk epilogue, 8 = no VALU heads, 16 = no trunk LDS writes, 32 = no trunk barriers,
+// 64 = dX colour-head backward without its mask / weight math, 128 = dX without its point-major copies.
 #ifndef YANERF_ABLATE
 #define YANERF_ABLATE 0
 #endif
@@ -54,8 +55,14 @@ struct x3_t {};
 // weight-ring depth, occupancy target (waves per SIMD), operand planes, and the element types of the LDS tile,
 // of the saved activations / gradients in HBM and of the packed weights
 template <typename T> struct Cfg;
+#ifndef YANERF_BF16_PM
+#define YANERF_BF16_PM 1
+#endif
+// PM: saved activations / backward gradients stored point-major in per-section arrays ([Npad][width], written from the
+// LDS tile with 16-byte stores, read by the dW kernel with transposed LDS reads) instead of feature-major rows
 template <> struct Cfg<float> {
   static constexpr int M = 64, WAVES = 4, DXWAVES = 4, EPC = 4, KB = 16, APREF = 1, LOWREG = 0, WPE = 2, PLANES = 1;
+  static constexpr bool PM = false;
   typedef float lds_t;
   typedef float st_t;
   typedef float w_t;
@@ -64,6 +71,7 @@ template <> struct Cfg<bf16_t> {
   static constexpr int M = 128, WAVES = YANERF_BF16_WAVES, DXWAVES = YANERF_BF16_DXWAVES, EPC = 8, KB = 32,
                        APREF = YANERF_BF16_WAVES == 4 ? 2 : 3, LOWREG = YANERF_LOWREG, WPE = LOWREG ? 4 : 2;
   static constexpr int PLANES = 1;
+  static constexpr bool PM = YANERF_BF16_PM;
   typedef bf16_t lds_t;
   typedef bf16_t st_t;
   typedef bf16_t w_t;
@@ -74,6 +82,7 @@ template <> struct Cfg<bf16_t> {
 template <> struct Cfg<x3_t> {
   static constexpr int M = 64, WAVES = 8, DXWAVES = 8, EPC = 8, KB = 32, APREF = YANERF_X3_APREF, LOWREG = 0, WPE = 2,
                        PLANES = 3;
+  static constexpr bool PM = false;
   typedef bf16_t lds_t;
   typedef float st_t;
   typedef bf16_t w_t;
@@ -126,15 +135,18 @@ __host__ __device__ inline SavedRows saved_rows(int L) {
 struct GradRows {
   int64_t dz0, dyx, dzc, du, rows;
 };
-__host__ __device__ inline GradRows grad_rows(int L) {
+__host__ __device__ inline GradRows grad_rows(int L, bool pm = false) {
   GradRows g;
   g.dz0 = 0;
-  g.dyx = 256LL * L;  // 256 rows dY + 1 row dsigma
-  g.dzc = g.dyx + 257;
-  g.du = g.dzc + HC;
+  g.dyx = 256LL * L;  // feature-major: 256 rows dY + 1 row dsigma; point-major: dY [Npad][256] (dsigma in dU)
+  g.dzc = g.dyx + (pm ? 256 : 257);
+  g.du = g.dzc + HC;  // point-major dU [Npad][16]: du_j at column j, dsigma at column PM_DSIG
   g.rows = g.du + 16;
   return g;
 }
+constexpr int PM_DSIG = 8;
+// Point-major (Cfg::PM) storage: the section that starts at feature-row r0 (saved_rows / grad_rows offsets) with width
+// w is an [Npad][w] array at element r0 * Npad; element (point p, column c) at r0 * Npad + p * w + c.
 
 // ReLU masks, kept for the dX kernel instead of re-reading the saved activations:
 //  * trunk layers: the forward and dX kernels share one wave->tile decomposition (Cfg<T>), so every lane packs
@@ -169,8 +181,8 @@ __host__ __device__ inline int64_t row_ld(int64_t Npad, size_t es) {
   if ((units & 1) == 0) ++units;
   return units * 256 / (int64_t)es;
 }
-static int64_t saved_t_bytes(int L, int64_t Npad, size_t es) {
-  return saved_rows(L).rows * row_ld(Npad, es) * (int64_t)es;
+static int64_t saved_t_bytes(int L, int64_t Npad, size_t es, bool pm) {
+  return saved_rows(L).rows * (pm ? Npad : row_ld(Npad, es)) * (int64_t)es;
 }
 
 static int64_t tile_m(int prec) {
@@ -182,6 +194,9 @@ static size_t elem_size(int prec) { return prec == YANERF_PREC_BF16 ? 2 : 4; }
 // element size and plane count of the packed GEMM operands
 static size_t w_size(int prec) { return prec == YANERF_PREC_F32 ? 4 : 2; }
 static int w_planes(int prec) { return prec == YANERF_PREC_F32X3 ? 3 : 1; }
+static bool prec_pm(int prec) {
+  return prec == YANERF_PREC_F32 ? Cfg<float>::PM : prec == YANERF_PREC_BF16 ? Cfg<bf16_t>::PM : Cfg<x3_t>::PM;
+}
 
 static int check_desc(const yanerf_mlp_desc* d) {
   YN_CHECK(d, "mlp: null desc");
@@ -869,6 +884,42 @@ __device__ __forceinline__ void store_mask_tile(uint64_t* masks, int64_t Npad, i
   if (lane < 4) masks[mask_index(Npad, slot, pt16, ft) + lane] = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
 }
 
+// Point-major (Cfg::PM) save: columns [col0, col0 + W) of the LDS tile's M points -> the [Npad][W] section at
+// dst = section + p0 * W. A lane moves one 16-byte chunk: a 16-lane group reads 256 contiguous bytes of one LDS row
+// (the row swizzle permutes chunks within aligned groups of 8) and a wave-instruction writes 1 KiB contiguously.
+template <typename T, int NTHR, int W>
+__device__ __forceinline__ void copy_tile_pm(const typename Cfg<T>::lds_t* act, int col0, typename Cfg<T>::st_t* dst,
+                                             int tid) {
+  static_assert(sizeof(typename Cfg<T>::st_t) == 2 && !is_x3<T>, "point-major save: bf16 tiles");
+  constexpr int M = Cfg<T>::M, CPR = W / 8, TOT = M * CPR, IT = TOT / NTHR;
+  static_assert(TOT % NTHR == 0, "copy_tile_pm: whole chunks per thread");
+  constexpr int GRP = IT < 4 ? IT : 4;  // chunks in flight per lane (bounds the live registers)
+  // an opaque copy of tid: the address arithmetic below is redone at every call instead of being hoisted out of the
+  // caller's layer loop (where its 2 x IT address registers would be live across every GEMM)
+  int t = tid;
+  asm volatile("" : "+v"(t));
+  // global side: a buffer resource on the section (uniform) + one 32-bit lane offset; chunk i is NTHR * 16 bytes on
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
+  const int m0 = t / CPR, c = t % CPR;
+  const uint32_t goff = (uint32_t)(t * 16);
+  static_assert(NTHR % CPR == 0, "copy_tile_pm: whole rows per pass");
+#pragma unroll
+  for (int i0 = 0; i0 < IT; i0 += GRP) {
+    f4 v[GRP];
+#pragma unroll
+    for (int i = 0; i < GRP; ++i) v[i] = lds_chunk<T>(act, m0 + (NTHR / CPR) * (i0 + i), col0 / 8 + c);
+#pragma unroll
+    for (int i = 0; i < GRP; ++i)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint32_t __attribute__((ext_vector_type(4))), v[i]), rs,
+                                             goff, (i0 + i) * NTHR * 16, 0);
+  }
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global stores (the
+// saved rows / gradients / masks written between barriers are read by later kernels only). __syncthreads() is a
+// workgroup fence as well and waits for every outstanding store (vmcnt(0)) at each of the ~24 barriers per tile.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // ============================================================================================ forward
 // SAVE: training forward (saved activation rows + ReLU masks for the backward); else inference, outputs only.
 template <typename T, bool SAVE>
@@ -913,16 +964,23 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   float x3[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) x3[i] = o3[i] + t * d3[i];  // models/utils.py:244
+  constexpr bool PM = Cfg<T>::PM;
+  constexpr int NTHR = WAVES * 64;
   if (!(YANERF_ABLATE & 2))
     harmonic_to_lds<T>(act, mt_, PE_COL, KPE, x3, lay.fx, lay.ax, q,
-                       saved ? saved + SR.pe * ld + p : nullptr, ld);
-  __syncthreads();
+                       (saved && !PM) ? saved + SR.pe * ld + p : nullptr, ld);
+  lds_barrier();
 
   f4 acc[NT][MT];
   const int nrow0 = wave * NT * 16;
   // weight ring of the next GEMM, filled before the current layer's epilogue (bf16; no-op for fp32)
   ARing<T, NT> ring;
   ring_fill<T, NT>(ring, Wt + lay.w_off[0], wpl, lay.kpad[0], nrow0, KPE / KB, lane);
+  // point-major saves are issued AFTER the following GEMM (and its next-ring loads): loads and stores share vmcnt
+  // and complete in order, so a store issued before a GEMM's weight loads makes every wait on those loads wait for
+  // the store's write acknowledgement too. The GEMM of layer l + 1 still reads H_l from the LDS tile, so H_l (and the
+  // mask words of layer l) leave during iteration l + 1, between its GEMM and its epilogue barrier.
+  uint64_t pbits[MW] = {};
   for (int l = 0; l < lay.L; ++l) {
     const bool sk = (lay.skip >> l) & 1u;
     const int kc0 = (l == 0) ? PE_COL / EPC : 0;
@@ -932,7 +990,19 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     if (l + 1 < lay.L)
       ring_fill<T, NT>(ring, Wt + lay.w_off[l + 1], wpl, lay.kpad[l + 1], nrow0, lay.kpad[l + 1] / KB, lane);
     else ring_fill<T, NT>(ring, Wt + lay.wint_off, wpl, 256, nrow0, 256 / KB, lane);
-    if (!(YANERF_ABLATE & 32)) __syncthreads();
+    if constexpr (PM) {
+      if (sv && !(YANERF_ABLATE & 4)) {
+        if (l == 0) {
+          copy_tile_pm<T, NTHR, KPE>(act, PE_COL, saved + SR.pe * Npad + p0 * KPE, tid);
+        } else {
+          copy_tile_pm<T, NTHR, 256>(act, 0, saved + (SR.h0 + 256LL * (l - 1)) * Npad + p0 * 256, tid);
+#pragma unroll
+          for (int w = 0; w < MW; ++w)
+            masks[((((int64_t)(l - 1) * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
+        }
+      }
+    }
+    if (!(YANERF_ABLATE & 32)) lds_barrier();
     uint64_t bits[MW] = {};
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -944,17 +1014,22 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
         if (!(YANERF_ABLATE & 16)) pk_lds<T>(act, m, n, h);
         else if (__float_as_uint(acc[nt][mt].x) == 0x7fc00001u) act[m] = (LT)0;  // keep acc live
         if (sv && !(YANERF_ABLATE & 4)) {
-          pk_store_rows_b<T>((saved + (SR.h0 + 256LL * l + nrow0 + 16 * nt) * ld + p0),
+          if constexpr (!PM)
+            pk_store_rows_b<T>((saved + (SR.h0 + 256LL * l + nrow0 + 16 * nt) * ld + p0),
                                soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
           mask_acc(bits, h, nt * MT + mt);
         }
       }
     }
-    if (sv && !(YANERF_ABLATE & 4))
+    if constexpr (PM) {
+#pragma unroll
+      for (int w = 0; w < MW; ++w) pbits[w] = bits[w];
+    } else if (sv && !(YANERF_ABLATE & 4)) {
 #pragma unroll
       for (int w = 0; w < MW; ++w)
         masks[((((int64_t)l * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane] = bits[w];
-    if (!(YANERF_ABLATE & 32)) __syncthreads();
+    }
+    if (!(YANERF_ABLATE & 32)) lds_barrier();
   }
   // ---- density head: sigma = w_d . h + b_d (nerf_mlp.py:173; density_layer 256->1) as one 16-row MFMA tile per
   // 16-point group (rows past 0 are zero weights); wave w takes groups w, w + WAVES, ...; lanes g == 0 hold sigma of
@@ -976,7 +1051,15 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   const int crow0 = wave * NTC * 16;
   ARing<T, NTC> ringc;
   ring_fill<T, NTC>(ringc, Wt + lay.wc_off, wpl, KC, crow0, KC / KB, lane);
-  __syncthreads();
+  if constexpr (PM) {
+    if (sv && !(YANERF_ABLATE & 4)) {
+      copy_tile_pm<T, NTHR, 256>(act, 0, saved + (SR.h0 + 256LL * (lay.L - 1)) * Npad + p0 * 256, tid);
+#pragma unroll
+      for (int w = 0; w < MW; ++w)
+        masks[((((int64_t)(lay.L - 1) * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
+    }
+  }
+  lds_barrier();
   {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -987,7 +1070,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
         const int m = 16 * mt + li;
         const Pk<T> h = pk_make<T>(v);
         pk_lds<T>(act, m, n, h);
-        if (sv) pk_store_rows_b<T>((saved + (SR.y + nrow0 + 16 * nt) * ld + p0),
+        if (sv && !PM) pk_store_rows_b<T>((saved + (SR.y + nrow0 + 16 * nt) * ld + p0),
                              soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
       }
     }
@@ -998,14 +1081,20 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     float dn[3] = {d3[0] / nrm, d3[1] / nrm, d3[2] / nrm};
     if (!(YANERF_ABLATE & 2))
       harmonic_to_lds<T>(act, mt_, PE_COL, KDIR, dn, lay.fd, lay.ad, q,
-                         saved ? saved + SR.dpe * ld + p : nullptr, ld);
+                         (saved && !PM) ? saved + SR.dpe * ld + p : nullptr, ld);
   }
-  __syncthreads();
+  lds_barrier();
   // ---- color layer: LinearWithRepeat(256 + 27 -> 128) + ReLU as one K = 288 GEMM over [Y, dirPE]
   {
     f4 accc[NTC][MT];
     gemm_lds<T, NTC, MT>(Wt + lay.wc_off, wpl, KC, crow0, act, 0, KC / KB, accc, lane, Wf + lay.bc_off, &ringc);
-    __syncthreads();
+    if constexpr (PM) {
+      if (sv) {
+        copy_tile_pm<T, NTHR, 256>(act, 0, saved + SR.y * Npad + p0 * 256, tid);
+        copy_tile_pm<T, NTHR, KDIR>(act, PE_COL, saved + SR.dpe * Npad + p0 * KDIR, tid);
+      }
+    }
+    lds_barrier();
 #pragma unroll
     for (int nt = 0; nt < NTC; ++nt) {
       const int n = crow0 + 16 * nt + 4 * g;
@@ -1017,7 +1106,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
         const Pk<T> h = pk_make<T>(v);
         pk_lds<T>(act, m, n, h);
         if (sv) {
-          pk_store_rows_b<T>((saved + (SR.c + crow0 + 16 * nt) * ld + p0), soff, (int)ldb,
+          if constexpr (!PM)
+            pk_store_rows_b<T>((saved + (SR.c + crow0 + 16 * nt) * ld + p0), soff, (int)ldb,
                                16 * mt * (int)sizeof(ST), h);
           store_mask_tile(masks + (int64_t)lay.L * trunk_mask_words<T>(Npad), Npad, 0, p0 / 16 + mt,
                           (crow0 + 16 * nt) / 16, v, lane);
@@ -1025,7 +1115,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   // ---- output layer 128 -> color_dim + sigmoid, as for the density head (nerf_mlp.py:169-171)
 #pragma unroll
   for (int hg = 0; hg < HG; ++hg) {
@@ -1045,6 +1135,9 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
         }
       }
     }
+  }
+  if constexpr (PM) {
+    if (sv) copy_tile_pm<T, NTHR, HC>(act, 0, saved + SR.c * Npad + p0 * HC, tid);  // C is still in the tile
   }
 }
 
@@ -1074,7 +1167,9 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
   const int64_t ld = row_ld(Npad, sizeof(ST)), ldb = ld * (int64_t)sizeof(ST);
   const uint32_t soff = (uint32_t)(4 * g * ldb + li * (int64_t)sizeof(ST));  // this lane's offset in a row tile
   const int64_t wpl = lay.t_plane;
-  const GradRows GR = grad_rows(lay.L);
+  constexpr bool PM = Cfg<T>::PM;
+  constexpr int NTHR = WAVES * 64;
+  const GradRows GR = grad_rows(lay.L, PM);
   const int mt_ = tid / TPP, q = tid % TPP;
   const int64_t p = p0 + mt_;
   const bool valid = p < N;
@@ -1089,8 +1184,13 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
     }
   }
   if (q == 0) {
-    for (int j = 0; j < cd; ++j) grad[(GR.du + j) * ld + p] = to_st<T>(du[j]);
-    grad[(GR.dyx + 256) * ld + p] = to_st<T>(gs);
+    if constexpr (PM) {
+      for (int j = 0; j < cd; ++j) grad[GR.du * Npad + p * 16 + j] = to_st<T>(du[j]);
+      grad[GR.du * Npad + p * 16 + PM_DSIG] = to_st<T>(gs);
+    } else {
+      for (int j = 0; j < cd; ++j) grad[(GR.du + j) * ld + p] = to_st<T>(du[j]);
+      grad[(GR.dyx + 256) * ld + p] = to_st<T>(gs);
+    }
   }
   {
     const float* wo = Wf + lay.wo_off;
@@ -1114,18 +1214,22 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
         // feature cl within its 16-feature tile: ballot word cl & 3, bit 16 * (cl >> 2) + point
         const bool on = (cw[t][cl & 3] >> (16 * (cl >> 2) + (mt_ & 15))) & 1ull;
         float dz = on ? dc : 0.0f;
+        if constexpr ((YANERF_ABLATE & 64) != 0) dz = (float)c;
         lds_put1<T>(act, mt_, c, dz);
-        grad[(GR.dzc + c) * ld + p] = to_st<T>(dz);
+        if constexpr (!PM) grad[(GR.dzc + c) * ld + p] = to_st<T>(dz);
       }
   }
-  __syncthreads();
+  lds_barrier();
   f4 acc[NT][MT];
   const int nrow0 = wave * NT * 16;
   // ---- dY = Wc[:, :256]^T dZc   (K = 128)
   gemm_lds<T, NT, MT>(Wt + lay.wcT_off, wpl, HC, nrow0, act, 0, HC / KB, acc, lane);
   ARing<T, NT> ring;  // next GEMM's weights, fetched during the epilogue (bf16)
   ring_fill<T, NT>(ring, Wt + lay.wintT_off, wpl, 256, nrow0, 256 / KB, lane);
-  __syncthreads();
+  // point-major gradients leave the LDS tile after the GEMM that reads them (and its next-ring loads): see the
+  // forward's trunk loop on the shared, in-order vmcnt
+  if constexpr (PM) copy_tile_pm<T, NTHR, HC>(act, 0, grad + GR.dzc * Npad + p0 * HC, tid);
+  lds_barrier();
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int n = nrow0 + 16 * nt + 4 * g;
@@ -1135,11 +1239,12 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
       f4 v = acc[nt][mt];
       const Pk<T> h = pk_make<T>(v);
       pk_lds<T>(act, m, n, h);
-      pk_store_rows_b<T>((grad + (GR.dyx + nrow0 + 16 * nt) * ld + p0),
+      if constexpr (!PM)
+        pk_store_rows_b<T>((grad + (GR.dyx + nrow0 + 16 * nt) * ld + p0),
                              soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
     }
   }
-  __syncthreads();
+  lds_barrier();
   // ---- dH_{L-1} = Wint^T dY + w_d (x) dsigma ; dZ_{L-1} = dH * [H_{L-1} > 0]
   for (int l = lay.L; l >= 1; --l) {
     // l == L: the heads -> last trunk layer; else trunk layer l -> layer l-1
@@ -1151,7 +1256,11 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
       bits[w] = masks[((((int64_t)hl * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane];
     gemm_lds<T, NT, MT>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring);
     if (l - 1 >= 1) ring_fill<T, NT>(ring, Wt + lay.wt_off[l - 1], wpl, 256, nrow0, 256 / KB, lane);
-    __syncthreads();
+    if constexpr (PM && !(YANERF_ABLATE & 128)) {  // the GEMM's input: dY (l == L) or dZ_l
+      if (l == lay.L) copy_tile_pm<T, NTHR, 256>(act, 0, grad + GR.dyx * Npad + p0 * 256, tid);
+      else copy_tile_pm<T, NTHR, 256>(act, 0, grad + (GR.dz0 + 256LL * l) * Npad + p0 * 256, tid);
+    }
+    lds_barrier();
     const float* wd = Wf + lay.wd_off;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -1168,12 +1277,14 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
         // ReLU mask of H_{hl}: this lane's own bits of this tile (packed by the forward)
         const Pk<T> h = pk_make<T>(apply_mask_tile<T, MW>(v, bits, nt * MT + mt));
         pk_lds<T>(act, m, n, h);
-        pk_store_rows_b<T>((grad + (GR.dz0 + 256LL * hl + nrow0 + 16 * nt) * ld + p0),
+        if constexpr (!PM)
+          pk_store_rows_b<T>((grad + (GR.dz0 + 256LL * hl + nrow0 + 16 * nt) * ld + p0),
                              soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
+  if constexpr (PM && !(YANERF_ABLATE & 128)) copy_tile_pm<T, NTHR, 256>(act, 0, grad + GR.dz0 * Npad + p0 * 256, tid);
 }
 
 // ============================================================================================ backward dW
@@ -1200,6 +1311,10 @@ struct DwJob {
   int64_t slab_off;
   float* W;  // grad of weight [a_rows][ktot] (reference layout)
   float* b;  // grad of bias [a_rows]
+  // point-major operands (Cfg::PM): A / X0 / X1 are [Npad][ld] sections (A already offset to its first column);
+  // a_chunks = 16-byte chunks of A per point that hold data; the tile's column space is "virtual": X0's columns
+  // padded to x0p (a multiple of 8), then X1's (ktot_v = x0p + x1_rows); k-tiles are laid over ktot_v
+  int a_ld, a_chunks, x0_ld, x1_ld, x0p, ktot_v;
 };
 constexpr int kMaxDwJobs = MAXL + 4;
 struct DwJobs {
@@ -1389,6 +1504,160 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
   }
 }
 
+// Point-major bf16 dW (Cfg::PM). A stage is 32 points (one 16x16x32 K-block): the A image [32 points][BN features]
+// and the X image [32 points][BK features], 2*BN / 2*BK bytes per point row, each filled by LDS-DMA from BN / BK
+// contiguous features of the point's row in its section (512-byte runs for 256-wide tiles). MFMA operands come
+// from the images with ds_read_b64_tr_b16: for lane group g (points 8g..8g+7) two transposed reads of 4 points x 16
+// features give the 8-point fragment of 16 features, for dZ^T (A, rows = output features) and X (B, columns).
+// 16-byte chunk c of image row r sits at chunk c ^ pm_swz(r): every transposed read is conflict-free (a 32-lane half
+// touches rows {r0..r0+3, r0+8..r0+11} x 2 chunks -> 16 distinct bank slots). Bias gradients ride along as an extra
+// MFMA against a ones fragment in the k-tile-0 workgroups (column sums over the points).
+template <int ROWB>
+__device__ __forceinline__ int pm_swz(int r) {
+  static_assert(ROWB == 128 || ROWB == 256 || ROWB == 512, "pm image row width");
+  if constexpr (ROWB == 128) return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
+  else return 2 * ((r & 3) | (((r >> 3) & 1) << 2));
+}
+constexpr int PM_SPTS = 32;  // points per dW stage
+typedef short s4v __attribute__((ext_vector_type(4)));
+// fragment of 16 features x 8 points (points 8g..8g+7 of the stage for lane group g) from an image with ROWB-byte rows
+template <int ROWB>
+__device__ __forceinline__ f4 pm_frag(const char* img, int f0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int c = f0 / 8 + (p >> 1);
+  f4 out;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int r = 8 * g + 4 * hh + q;
+    const char* a = img + r * ROWB + 16 * (c ^ pm_swz<ROWB>(r)) + 8 * (p & 1);
+    const s4v v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(a));
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v w = __builtin_bit_cast(f2v, v);
+    if (hh == 0) { out.x = w.x; out.y = w.y; } else { out.z = w.x; out.w = w.y; }
+  }
+  return out;
+}
+
+template <int BN, int BK>
+__device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S, int64_t Npad, float* __restrict__ slab,
+                                           int64_t slab_elems, char* smem) {
+  constexpr int WN = BN / 64, WK0 = 8 / WN, WK = (BK / 16 < WK0) ? BK / 16 : WK0, KTW = BK / WK / 16;
+  static_assert(KTW >= 1 && WN * WK <= 8, "dW wave tiling");
+  constexpr int AB = PM_SPTS * BN * 2, XB = PM_SPTS * BK * 2;  // image bytes
+  constexpr int NI = (AB + XB) / 1024, PW = (NI + 7) / 8;      // DMA wave-instructions per stage / per wave
+  static_assert(PW * 8 * 1024 <= DW_STAGE_BYTES, "pm dW stage");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int wn = wave / WK, wk = wave % WK;
+  const bool mma_wave = wave < WN * WK;
+  const int64_t nst = Npad / PM_SPTS;
+  const int64_t st_lo = nst * s / S, st_hi = nst * (s + 1) / S;
+  // this lane's DMA source per wave-instruction and its per-stage advance (32 points of its section)
+  const bf16_t* src[PW];
+  int64_t adv[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int ii = 8 * i + wave;
+    const int b = (ii < NI ? ii : 0) * 1024 + lane * 16;
+    if (b < AB) {
+      const int r = b / (2 * BN), c = ((b % (2 * BN)) / 16) ^ pm_swz<2 * BN>(r);
+      src[i] = (const bf16_t*)J.A + (int64_t)r * J.a_ld + 8 * (c < J.a_chunks ? c : 0);
+      adv[i] = (int64_t)PM_SPTS * J.a_ld;
+    } else {
+      const int bx = b - AB, r = bx / (2 * BK), c = ((bx % (2 * BK)) / 16) ^ pm_swz<2 * BK>(r);
+      const int j = k0 + 8 * c;  // virtual column
+      if (j < J.x0p) {
+        src[i] = (const bf16_t*)J.X0 + (int64_t)r * J.x0_ld + j;
+        adv[i] = (int64_t)PM_SPTS * J.x0_ld;
+      } else if (j - J.x0p < J.x1_ld && J.X1) {
+        src[i] = (const bf16_t*)J.X1 + (int64_t)r * J.x1_ld + (j - J.x0p);
+        adv[i] = (int64_t)PM_SPTS * J.x1_ld;
+      } else {  // past the virtual width: any valid address (never stored)
+        src[i] = (const bf16_t*)J.X0 + (int64_t)r * J.x0_ld;
+        adv[i] = (int64_t)PM_SPTS * J.x0_ld;
+      }
+    }
+  }
+  auto issue = [&](int64_t st) {
+    char* dst = smem + (int)(st % DW_STAGES) * DW_STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+      __builtin_amdgcn_global_load_lds(src[i] + st * adv[i],
+                                       (__attribute__((address_space(3))) void*)(dst + (8 * i + wave) * 1024), 16, 0, 0);
+  };
+  const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = (k0 == 0) && wk == 0;
+  const float one2 = __uint_as_float(0x3f803f80u);  // two bf16 1.0 halves
+  const f4 ones = f4{one2, one2, one2, one2};
+  f4 acc[4][KTW], accb[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    accb[nt] = zero;
+#pragma unroll
+    for (int q = 0; q < KTW; ++q) acc[nt][q] = zero;
+  }
+#pragma unroll
+  for (int i = 0; i < DW_STAGES - 1; ++i)
+    if (st_lo + i < st_hi) issue(st_lo + i);
+  for (int64_t st = st_lo; st < st_hi; ++st) {
+    const int64_t ahead = st_hi - 1 - st;
+    static_assert(DW_STAGES == 4, "wait ladder below");
+    if (ahead >= DW_STAGES - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (DW_STAGES - 2)) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (st + DW_STAGES - 1 < st_hi) issue(st + DW_STAGES - 1);
+    const char* buf = smem + (int)(st % DW_STAGES) * DW_STAGE_BYTES;
+    if (mma_wave) {
+      f4 a[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) a[nt] = pm_frag<2 * BN>(buf, wn * 64 + 16 * nt, lane);
+      constexpr int QG = KTW < 4 ? KTW : 4;
+#pragma unroll
+      for (int q0 = 0; q0 < KTW; q0 += QG) {
+        f4 b[QG];
+#pragma unroll
+        for (int q = 0; q < QG; ++q) b[q] = pm_frag<2 * BK>(buf + AB, (wk * KTW + q0 + q) * 16, lane);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int q = 0; q < QG; ++q) acc[nt][q0 + q] = mma_blk<bf16_t>(a[nt], b[q], acc[nt][q0 + q]);
+      }
+      if (do_bias) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) accb[nt] = mma_blk<bf16_t>(a[nt], ones, accb[nt]);
+      }
+    }
+  }
+  float* out = slab + (int64_t)s * slab_elems + J.slab_off;
+  const int kv = J.ktot + 1;
+  if (mma_wave) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int q = 0; q < KTW; ++q) {
+        const int j = k0 + (wk * KTW + q) * 16 + li;  // virtual column -> weight column
+        const int k = j < J.x0p ? (j < J.x0_rows ? j : -1) : (j - J.x0p < J.x1_rows ? J.x0_rows + j - J.x0p : -1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = wn * 64 + 16 * nt + 4 * g + r;
+          if (n < J.a_rows && k >= 0) out[(int64_t)n * kv + k] = acc[nt][q][r];
+        }
+      }
+    if (do_bias && li == 0) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = wn * 64 + 16 * nt + 4 * g + r;
+          if (n < J.a_rows) out[(int64_t)n * kv + J.ktot] = accb[nt][r];
+        }
+    }
+  }
+}
+
 // x3 dW: dZ and the layer inputs are fp32 rows in HBM (the x3 forward / dX save fp32). Each stage of 32 points is
 // loaded with 16-byte register loads (4 points of one row per thread-load, the next stage in flight while the
 // current one multiplies), split into three bf16 planes on the way into LDS (same 64-byte rows and swizzle as the
@@ -1539,7 +1808,20 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   const int k0 = kt * BKMAX;
   const int bk = kt < J.k_full ? BKMAX : J.bk_tail;
   const int64_t se = jobs.slab_elems;
-  if constexpr (is_x3<T>) {
+  if constexpr (Cfg<T>::PM) {
+    if (J.bn == 256) {
+      if (bk == 256) dw_tile_pm<256, 256>(J, k0, s, S, Npad, slab, se, smem);
+      else if (bk == 128) dw_tile_pm<256, 128>(J, k0, s, S, Npad, slab, se, smem);
+      else dw_tile_pm<256, 64>(J, k0, s, S, Npad, slab, se, smem);
+    } else if (J.bn == 128) {
+      if (bk == 256) dw_tile_pm<128, 256>(J, k0, s, S, Npad, slab, se, smem);
+      else if (bk == 128) dw_tile_pm<128, 128>(J, k0, s, S, Npad, slab, se, smem);
+      else dw_tile_pm<128, 64>(J, k0, s, S, Npad, slab, se, smem);
+    } else {
+      if (bk == 256) dw_tile_pm<64, 256>(J, k0, s, S, Npad, slab, se, smem);
+      else dw_tile_pm<64, 128>(J, k0, s, S, Npad, slab, se, smem);
+    }
+  } else if constexpr (is_x3<T>) {
     if (J.bn == 256) {
       if (bk == 128) dw_tile_x3<256, 128>(J, k0, s, S, Npad, slab, se, smem);
       else dw_tile_x3<256, 64>(J, k0, s, S, Npad, slab, se, smem);
@@ -1644,59 +1926,80 @@ static void dw_ktiles(int ktot, int bn, int prec, int* k_full, int* bk_tail, int
   *k_tiles = *k_full + (rem > 0 ? 1 : 0);
 }
 
-// enumerate the dW jobs (shared by the size query and the launch)
+// enumerate the dW jobs (shared by the size query and the launch): A = the gradient rows / section (first row,
+// rows, section width, first column), X0 / X1 = the layer-input rows / sections (first row, rows, section width)
+struct DwSpec {
+  int64_t arow;
+  int a_rows, a_w, a_col;
+  int64_t x0;
+  int x0_rows, x0_w;
+  int64_t x1;
+  int x1_rows, x1_w;
+  int gi;
+};
 template <typename F>
-static void for_each_dw_job(const MlpLayout& L, F&& f) {
+static void for_each_dw_job(const MlpLayout& L, bool pm, F&& f) {
   const SavedRows SR = saved_rows(L.L);
-  const GradRows GR = grad_rows(L.L);
+  const GradRows GR = grad_rows(L.L, pm);
   for (int l = 0; l < L.L; ++l) {
     const int nout = (l + 1 < L.L) ? 256 : L.hid;
     const bool sk = (L.skip >> l) & 1u;
-    if (l == 0) f(GR.dz0, nout, SR.pe, L.xyz_dim, -1, 0, 2 * l);
-    else if (sk) f(GR.dz0 + 256LL * l, nout, SR.h0 + 256LL * (l - 1), 256, SR.pe, L.xyz_dim, 2 * l);
-    else f(GR.dz0 + 256LL * l, nout, SR.h0 + 256LL * (l - 1), 256, -1, 0, 2 * l);
+    if (l == 0) f(DwSpec{GR.dz0, nout, 256, 0, SR.pe, L.xyz_dim, KPE, -1, 0, 0, 2 * l});
+    else if (sk)
+      f(DwSpec{GR.dz0 + 256LL * l, nout, 256, 0, SR.h0 + 256LL * (l - 1), 256, 256, SR.pe, L.xyz_dim, KPE, 2 * l});
+    else f(DwSpec{GR.dz0 + 256LL * l, nout, 256, 0, SR.h0 + 256LL * (l - 1), 256, 256, -1, 0, 0, 2 * l});
   }
   // heaviest jobs first: the grid is dispatched in job order, so the light ones fill the last round
   const int h = 2 * L.L;
-  f(GR.dyx, L.hid, SR.h0 + 256LL * (L.L - 1), L.hid, -1, 0, h + 0);        // intermediate_linear
-  f(GR.dzc, L.hdir, SR.y, L.hid, SR.dpe, L.dir_dim, h + 4);               // color_layer.0 (LinearWithRepeat)
-  f(GR.dyx + 256, 1, SR.h0 + 256LL * (L.L - 1), L.hid, -1, 0, h + 2);      // density_layer
-  f(GR.du, L.cdim, SR.c, L.hdir, -1, 0, h + 6);                           // color_layer.2
+  const int64_t hl = SR.h0 + 256LL * (L.L - 1);
+  f(DwSpec{GR.dyx, L.hid, 256, 0, hl, L.hid, 256, -1, 0, 0, h + 0});                      // intermediate_linear
+  f(DwSpec{GR.dzc, L.hdir, HC, 0, SR.y, L.hid, 256, SR.dpe, L.dir_dim, KDIR, h + 4});     // color_layer.0
+  if (pm) f(DwSpec{GR.du, 1, 16, PM_DSIG, hl, L.hid, 256, -1, 0, 0, h + 2});             // density_layer
+  else f(DwSpec{GR.dyx + 256, 1, 256, 0, hl, L.hid, 256, -1, 0, 0, h + 2});
+  f(DwSpec{GR.du, L.cdim, 16, 0, SR.c, L.hdir, HC, -1, 0, 0, h + 6});                    // color_layer.2
 }
 
 static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void* gradbuf, int64_t Npad,
                           float* const* grads, DwJobs& D) {
   const size_t es = elem_size(prec);
-  const int64_t ld = row_ld(Npad, es);
+  const bool pm = prec_pm(prec);
+  const int64_t ld = pm ? Npad : row_ld(Npad, es);
   auto srow = [&](int64_t r) { return r < 0 ? nullptr : (const void*)((const char*)saved + r * ld * es); };
   auto grow = [&](int64_t r) { return (const void*)((const char*)gradbuf + r * ld * es); };
   D.n = 0;
   D.total_tiles = 0;
   D.slab_elems = 0;
-  for_each_dw_job(L, [&](int64_t arow, int a_rows, int64_t x0, int x0_rows, int64_t x1, int x1_rows, int gi) {
+  for_each_dw_job(L, pm, [&](const DwSpec& sp) {
     DwJob& j = D.j[D.n++];
-    j.A = grow(arow); j.a_rows = a_rows;
-    j.X0 = srow(x0); j.x0_rows = x0_rows; j.X1 = srow(x1); j.x1_rows = x1_rows;
-    j.ktot = x0_rows + x1_rows;
-    j.bn = dw_bn(a_rows);
-    dw_ktiles(j.ktot, j.bn, prec, &j.k_full, &j.bk_tail, &j.k_tiles);
+    j.A = grow(sp.arow); j.a_rows = sp.a_rows;
+    j.X0 = srow(sp.x0); j.x0_rows = sp.x0_rows; j.X1 = srow(sp.x1); j.x1_rows = sp.x1_rows;
+    j.ktot = sp.x0_rows + sp.x1_rows;
+    j.a_ld = sp.a_w; j.x0_ld = sp.x0_w; j.x1_ld = sp.x1_w;
+    if (pm) j.A = (const char*)j.A + (int64_t)sp.a_col * es;
+    j.a_chunks = (sp.a_w - sp.a_col) / 8;
+    j.x0p = pm ? (sp.x0_rows + 7) / 8 * 8 : sp.x0_rows;
+    j.ktot_v = j.x0p + sp.x1_rows;
+    j.bn = dw_bn(sp.a_rows);
+    dw_ktiles(j.ktot_v, j.bn, prec, &j.k_full, &j.bk_tail, &j.k_tiles);
     j.tile_base = D.total_tiles;
     D.total_tiles += j.k_tiles;
     j.slab_off = D.slab_elems;
-    D.slab_elems += (int64_t)a_rows * (j.ktot + 1);
-    j.W = grads[gi];
-    j.b = grads[gi + 1];
+    D.slab_elems += (int64_t)sp.a_rows * (j.ktot + 1);
+    j.W = grads[sp.gi];
+    j.b = grads[sp.gi + 1];
   });
 }
 
 static int64_t dw_slab_elems_for(const MlpLayout& L, int prec, int* total_tiles) {
   int64_t e = 0;
   int tiles = 0;
-  for_each_dw_job(L, [&](int64_t, int a_rows, int64_t, int x0_rows, int64_t, int x1_rows, int) {
-    const int ktot = x0_rows + x1_rows;
-    e += (int64_t)a_rows * (ktot + 1);
+  const bool pm = prec_pm(prec);
+  for_each_dw_job(L, pm, [&](const DwSpec& sp) {
+    const int ktot = sp.x0_rows + sp.x1_rows;
+    const int ktot_v = (pm ? (sp.x0_rows + 7) / 8 * 8 : sp.x0_rows) + sp.x1_rows;
+    e += (int64_t)sp.a_rows * (ktot + 1);
     int kf, bt, kt;
-    dw_ktiles(ktot, dw_bn(a_rows), prec, &kf, &bt, &kt);
+    dw_ktiles(ktot_v, dw_bn(sp.a_rows), prec, &kf, &bt, &kt);
     tiles += kt;
   });
   if (total_tiles) *total_tiles = tiles;
@@ -1714,7 +2017,7 @@ static int launch_fwd(const MlpLayout& L, int prec, const void* packed, const fl
   const typename Cfg<T>::w_t* Wt = (const typename Cfg<T>::w_t*)packed;
   const float* Wf = (const float*)((const char*)packed + L.f_base);
   dim3 grid((unsigned)(Npad / Cfg<T>::M)), block(Cfg<T>::WAVES * 64);
-  uint64_t* masks = saved ? (uint64_t*)((char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST))) : nullptr;
+  uint64_t* masks = saved ? (uint64_t*)((char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM)) : nullptr;
   if (saved || !std::is_same<T, bf16_t>::value)
     hipLaunchKernelGGL((mlp_fwd_kernel<T, true>), grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, (ST*)saved,
                        saved ? masks : nullptr, Npad);
@@ -1732,11 +2035,11 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   const int64_t Npad = npad_of(prec, N);
   const typename Cfg<T>::w_t* Wt = (const typename Cfg<T>::w_t*)packed;
   const float* Wf = (const float*)((const char*)packed + L.f_base);
-  const GradRows GR = grad_rows(L.L);
+  const GradRows GR = grad_rows(L.L, Cfg<T>::PM);
   ST* gradbuf = (ST*)ws;
-  int64_t grad_bytes = GR.rows * row_ld(Npad, sizeof(ST)) * (int64_t)sizeof(ST);
+  int64_t grad_bytes = GR.rows * (Cfg<T>::PM ? Npad : row_ld(Npad, sizeof(ST))) * (int64_t)sizeof(ST);
   float* slab = (float*)((char*)ws + grad_bytes);
-  const uint64_t* masks = (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST)));
+  const uint64_t* masks = (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM));
   hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::DXWAVES * 64), 0, st, L, Wt,
                      Wf, masks, rgb, gs, gr, N, Npad, gradbuf);
   YN_LAUNCH_CHECK("mlp_backward_dx");
@@ -1791,7 +2094,7 @@ int yanerf_mlp_pack(const yanerf_mlp_desc* d, int precision, const float* const*
 int64_t yanerf_mlp_saved_bytes(const yanerf_mlp_desc* d, int precision, int64_t n_points) {
   if (check_desc(d)) return -1;
   const int64_t Npad = npad_of(precision, n_points);
-  return saved_t_bytes(d->n_layers, Npad, elem_size(precision)) +
+  return saved_t_bytes(d->n_layers, Npad, elem_size(precision), prec_pm(precision)) +
          (d->n_layers * trunk_mask_words_prec(precision, Npad) + mask_words_per_slot(Npad)) * 8;
 }
 
@@ -1799,8 +2102,9 @@ int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, 
   if (check_desc(d)) return -1;
   MlpLayout L = make_layout(d, precision);
   const int64_t Npad = npad_of(precision, n_points);
-  const GradRows GR = grad_rows(d->n_layers);
-  int64_t grad_bytes = GR.rows * row_ld(Npad, elem_size(precision)) * (int64_t)elem_size(precision);
+  const bool pm = prec_pm(precision);
+  const GradRows GR = grad_rows(d->n_layers, pm);
+  int64_t grad_bytes = GR.rows * (pm ? Npad : row_ld(Npad, elem_size(precision))) * (int64_t)elem_size(precision);
   int tiles = 0;
   int64_t se = dw_slab_elems_for(L, precision, &tiles);
   int S = dw_splits(tiles, Npad / dw_stage_pts(precision));

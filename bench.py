@@ -198,6 +198,7 @@ def main():
     rank, world, local = parallel.init_distributed()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    local = parallel.device_index(local)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cfg = Config.fromfile(args.config)

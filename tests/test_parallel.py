@@ -55,3 +55,53 @@ def test_gloo_world2():
     assert torch.allclose(g0, expect) and torch.allclose(g1, expect)
     assert torch.equal(m0, torch.tensor([0.0, 1.0])) and x0 == x1 == 1.5
     assert sorted(sum(s0, [])) == list(range(10))
+
+
+def _eval_worker(rank, world, port, q):
+    """Sharded evaluation plumbing: DistributedSampler split + per-iteration all_gather restores dataset order and
+    drops the padding (apis.py:173-177, 201); row shards of an image reassemble it exactly."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from yanerf_amd import parallel
+    parallel.init_distributed(backend="gloo")
+    n = 7  # not a multiple of the world size: the reference's sampler pads with the head of the list
+    per_image = torch.arange(n, dtype=torch.float32) * 0.5 + 1.0
+    got = [parallel.allgather_cat(per_image[i].view(1, 1)) for i in parallel.eval_order(n, rank, world)]
+    gathered = torch.cat(got, dim=0)[:n].view(-1)
+    H, W = 11, 5
+    img = torch.arange(H * W * 3, dtype=torch.float32).view(H, W, 3)
+    rows = parallel.shard_range(H, rank, world)
+    full = parallel.gather_rows(img[rows.start:rows.stop].clone(), H)
+    q.put((rank, gathered, full, parallel.world_rank()))
+    parallel.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_gloo_world3_sharded_eval():
+    world, port = 3, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_eval_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = torch.arange(7, dtype=torch.float32) * 0.5 + 1.0
+    img = torch.arange(11 * 5 * 3, dtype=torch.float32).view(11, 5, 3)
+    for rank, gathered, full, wr in res:
+        assert wr == (3, rank)
+        assert torch.equal(gathered, expect)
+        assert torch.equal(full, img)
+
+
+def test_eval_order_matches_distributed_sampler():
+    from torch.utils.data import DistributedSampler
+
+    from yanerf_amd import parallel
+    for n in (1, 5, 8, 13):
+        for world in (1, 2, 3, 8):
+            for rank in range(world):
+                ref = list(DistributedSampler(range(n), num_replicas=world, rank=rank, shuffle=False))
+                assert parallel.eval_order(n, rank, world) == ref

@@ -24,14 +24,25 @@ def init_distributed(backend: Optional[str] = None) -> tuple:
     Returns (rank, world_size, local_rank). world_size 1 -> no process group."""
     rank, world, local = env_rank_world()
     if world > 1 and not dist.is_initialized():
+        # YANERF_DIST_BACKEND=gloo: a rehearsal of the N-rank code path with several ranks on one card (RCCL needs one
+        # card per rank); the measured runs use the default, RCCL
+        backend = backend or os.environ.get("YANERF_DIST_BACKEND") or None
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
+            local = device_index(local)
             torch.cuda.set_device(local)
             dist.init_process_group(backend=backend, device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend=backend)
     return rank, world, local
+
+
+def device_index(local_rank: int) -> int:
+    """The card of a local rank: one card per rank; ranks beyond the visible cards (a one-card rehearsal of an
+    N-rank run) share them round-robin."""
+    n = torch.cuda.device_count()
+    return local_rank % n if n > 0 else local_rank
 
 
 def is_dist() -> bool:
@@ -58,8 +69,19 @@ def allgather_cat(x: torch.Tensor) -> torch.Tensor:
     if not is_dist():
         return x
     out = [torch.empty_like(x) for _ in range(dist.get_world_size())]
-    dist.all_gather(out, x.contiguous())
+    _all_gather(out, x.contiguous())
     return torch.cat(out, dim=0)
+
+
+def _all_gather(parts: List[torch.Tensor], x: torch.Tensor) -> None:
+    """all_gather that also runs under gloo with device tensors (CPU round trip; RCCL gathers in place)."""
+    if x.is_cuda and dist.get_backend() == "gloo":
+        host = [torch.empty_like(p, device="cpu") for p in parts]
+        dist.all_gather(host, x.cpu())
+        for p, h in zip(parts, host):
+            p.copy_(h)
+    else:
+        dist.all_gather(parts, x)
 
 
 def max_over_ranks(value: float, device=None) -> float:
@@ -80,6 +102,39 @@ def shard_range(n: int, rank: int, world: int) -> range:
     lo = n * rank // world
     hi = n * (rank + 1) // world
     return range(lo, hi)
+
+
+def world_rank() -> tuple:
+    """(world_size, rank) of the default group, (1, 0) without one."""
+    if is_dist():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def eval_order(n: int, rank: int, world: int) -> List[int]:
+    """The evaluation split of one rank: DistributedSampler(shuffle=False, drop_last=False) (runners/utils.py:
+    112-131) pads the index list to a multiple of the world size by repeating it from the head, then rank r takes
+    every world-th index from r. Gathering one item from every rank per iteration and concatenating the iterations
+    (apis.py:173-177) restores dataset order; the padding is cut off by the final [: len(dataset)] (apis.py:201)."""
+    total = -(-n // world) * world
+    order = list(range(n))
+    pad = total - n
+    order = order + (order * -(-pad // n))[:pad] if n else []
+    return order[rank:total:world]
+
+
+def gather_rows(local: torch.Tensor, n_total: int) -> torch.Tensor:
+    """Assemble a tensor sharded by `shard_range(n_total, rank, world)` along dim 0 on every rank: each shard is
+    padded to the largest shard's length, all-gathered, and the padding dropped. One collective per call."""
+    world, _ = world_rank()
+    if world == 1:
+        return local
+    cap = -(-n_total // world)
+    buf = local.new_zeros((cap,) + tuple(local.shape[1:]))
+    buf[: local.shape[0]] = local
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    _all_gather(parts, buf)
+    return torch.cat([parts[k][: len(shard_range(n_total, k, world))] for k in range(world)], dim=0)
 
 
 class FlatParams:

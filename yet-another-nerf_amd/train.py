@@ -221,11 +221,16 @@ class NeRFTrainer:
 
     @torch.no_grad()
     def render(self, pose: torch.Tensor, focal: torch.Tensor, H: Optional[int] = None, W: Optional[int] = None,
-               near: Optional[float] = None, far: Optional[float] = None, chunk: int = 65536):
+               near: Optional[float] = None, far: Optional[float] = None, chunk: int = 65536,
+               shard: bool = False):
         """Full-grid evaluation render of one camera with the current weights, on the fused inference kernels:
         the reference's EVALUATION pass (nerf_pipeline.py:217-236: FULL_GRID rays, deterministic depths and
         refinement, no density noise), in chunks of `chunk` rays (it chunks by 131072 points in Python; the result
-        does not depend on the chunking). Returns (rgb [H,W,C] fine, rgb [H,W,C] coarse, depth [H,W] fine)."""
+        does not depend on the chunking). Returns (rgb [H,W,C] fine, rgb [H,W,C] coarse, depth [H,W] fine).
+
+        shard=True (under torch.distributed): every rank renders its contiguous block of image rows
+        (parallel.shard_range) and one all_gather per output assembles the image on every rank. Rays are
+        independent, so the result equals the single-GPU render; there is no other exchange."""
         L = _C.lib()
         st = ops._stream()
         H = int(H or self.H)
@@ -237,8 +242,10 @@ class NeRFTrainer:
         for i, s in enumerate(self.specs):
             _C.check(L.yanerf_mlp_pack(ctypes.byref(s.desc()), s.precision, self.param_ptrs[i], _p(self.packed[i]),
                                        st), "yanerf_mlp_pack")
-        n = H * W
-        R = min(chunk, n)
+        world, rank = parallel.world_rank() if shard else (1, 0)
+        rows = parallel.shard_range(H, rank, world)
+        p0, n = rows.start * W, len(rows) * W
+        R = max(1, min(chunk, n))
         b = self._eval_buffers(R)
         C = self.specs[0].color_dim
         out_f = torch.empty(n, C, device=self.dev)
@@ -247,7 +254,7 @@ class NeRFTrainer:
         opts = self.march.opts(0, 0.0)
         for r0 in range(0, n, R):
             r = min(R, n - r0)
-            ids = torch.arange(r0, r0 + r, device=self.dev, dtype=torch.int64)
+            ids = torch.arange(p0 + r0, p0 + r0 + r, device=self.dev, dtype=torch.int64)
             seed, off = ops.RNG.next(r * self.Pc_eval)
             _C.check(L.yanerf_raygen(_p(pose), _p(focal), None, _p(ids), 1, r, W, H, float(self.W), float(self.H),
                                      near, far, self.Pc_eval, 2 if self.stratified_eval else 0, None, seed, off,
@@ -272,21 +279,29 @@ class NeRFTrainer:
             out_c[r0:r0 + r] = b["feats"][0, :r]
             out_f[r0:r0 + r] = b["feats"][1, :r]
             out_d[r0:r0 + r] = b["depth"][1, :r]
-        return out_f.view(H, W, C), out_c.view(H, W, C), out_d.view(H, W)
+        out_f, out_c, out_d = out_f.view(-1, W, C), out_c.view(-1, W, C), out_d.view(-1, W)
+        if world > 1:
+            out_f, out_c, out_d = (parallel.gather_rows(t, H) for t in (out_f, out_c, out_d))
+        return out_f, out_c, out_d
 
-    def evaluate(self, images) -> Dict[str, float]:
+    def evaluate(self, images, shard: bool = True) -> Dict[str, float]:
         """Render every camera of a DeviceImageSet and score it as the reference's eval_one_epoch + create_stats do:
-        per-image MSE of each stage (pipelines/utils.py:137-158), PSNR of the MEAN MSE (runners/utils.py:270-283)."""
-        mse_f, mse_c = [], []
-        for i in range(len(images)):
+        per-image MSE of each stage (pipelines/utils.py:137-158), PSNR of the MEAN MSE (runners/utils.py:270-283).
+        Under torch.distributed (shard=True) the images are split as the reference's evaluation DistributedSampler
+        splits them (parallel.eval_order) and the per-image MSEs are all-gathered per iteration (apis.py:173-177,
+        201), so every rank returns the same numbers as a single-GPU evaluation."""
+        world, rank = parallel.world_rank() if shard else (1, 0)
+        n = len(images)
+        mse = []
+        for i in parallel.eval_order(n, rank, world):
             pose, focal, img, nr, fr = images.item(i)
             near = None if nr is None else float(nr.mean())  # per-image bounds -> scalar (ray_sampler.py:280-283)
             far = None if fr is None else float(fr.mean())
             f, c, _ = self.render(pose, focal, images.H, images.W, near, far)
-            mse_f.append(torch.mean((f - img[0]) ** 2))
-            mse_c.append(torch.mean((c - img[0]) ** 2))
-        mf = float(torch.stack(mse_f).mean())
-        mc = float(torch.stack(mse_c).mean())
+            m = torch.stack([torch.mean((f - img[0]) ** 2), torch.mean((c - img[0]) ** 2)]).view(1, 2)
+            mse.append(parallel.allgather_cat(m) if world > 1 else m)
+        allm = torch.cat(mse, dim=0)[:n]  # dataset order; DistributedSampler padding dropped
+        mf, mc = (float(x) for x in allm.mean(dim=0).tolist())
         return {"loss_rgb_mse": mf, "loss_prev_stage_rgb_mse": mc, "loss_rgb_psnr": -10.0 * math.log10(max(mf, 1e-12)),
                 "loss_prev_stage_rgb_psnr": -10.0 * math.log10(max(mc, 1e-12))}
 

@@ -21,6 +21,8 @@
 // layer's pre-activation gradient dZ_l (feature-major, [row][point]); (2) a split-K dW kernel computes
 // dW_l = sum_points dZ_l x input_l (+ a virtual ones-row giving the bias gradient) into fp32 partial slabs,
 // (3) a deterministic reduce sums the slabs straight into the reference-layout parameter gradients.
+#include <type_traits>
+
 #include "common.hpp"
 
 // Development-only timing ablations (never set in the product build): 1 = no MFMA, 2 = no harmonic embedding,
@@ -31,13 +33,15 @@
 #endif
 // bf16 forward wave tile: 4 waves x (64 features x 128 points) -- half the LDS operand reads per MFMA of the 8-wave
 // (32 x 128) tiling, twice the accumulators; measured training forward 1.47 -> 1.26 ms, inference 0.92 -> 0.77 ms.
-// The dX kernel keeps 8 waves (its colour-head VALU work and 2-byte row stores want the wave count: 3.2 -> 3.8 ms
-// with 4). The ReLU-mask words the forward writes land in the dX kernel's layout either way (mask_w).
+// The dX kernel uses the same 4-wave tiling (two workgroups per CU: one's GEMM covers the other's store drain) since
+// its loop-invariant fragment addresses stopped spilling (gemm_run's opaque lane id) and its colour head writes whole
+// LDS chunks: fine-pass dX 1.40 (8 waves) -> 1.26 ms. The ReLU-mask words the forward writes land in the dX kernel's
+// layout either way (mask_w).
 #ifndef YANERF_BF16_WAVES
 #define YANERF_BF16_WAVES 4
 #endif
 #ifndef YANERF_BF16_DXWAVES
-#define YANERF_BF16_DXWAVES 8
+#define YANERF_BF16_DXWAVES 4
 #endif
 #ifndef YANERF_LOWREG
 #define YANERF_LOWREG 0
@@ -60,8 +64,15 @@ template <typename T> struct Cfg;
 #endif
 // PM: saved activations / backward gradients stored point-major in per-section arrays ([Npad][width], written from the
 // LDS tile with 16-byte stores, read by the dW kernel with transposed LDS reads) instead of feature-major rows
+#ifndef YANERF_F32_M
+#define YANERF_F32_M 64
+#endif
+#ifndef YANERF_F32_WPE
+#define YANERF_F32_WPE 2
+#endif
 template <> struct Cfg<float> {
-  static constexpr int M = 64, WAVES = 4, DXWAVES = 4, EPC = 4, KB = 16, APREF = 1, LOWREG = 0, WPE = 2, PLANES = 1;
+  static constexpr int M = YANERF_F32_M, WAVES = 4, DXWAVES = 4, EPC = 4, KB = 16, APREF = 1, LOWREG = 0,
+                       WPE = YANERF_F32_WPE, PLANES = 1;
   static constexpr bool PM = false;
   typedef float lds_t;
   typedef float st_t;
@@ -357,6 +368,43 @@ template <typename T> __device__ __forceinline__ void lds_put1(typename Cfg<T>::
     act[i] = f2bf(v);
   }
 }
+// write EPC consecutive values (one 16-byte chunk c of row m) into LDS in T's representation
+template <typename T>
+__device__ __forceinline__ void lds_put_chunk(typename Cfg<T>::lds_t* act, int m, int c, const float (&v)[Cfg<T>::EPC]) {
+  const int i = m * ROW + swz<T>(m, c) * Cfg<T>::EPC;
+  if constexpr (sizeof(typename Cfg<T>::lds_t) == 4) {
+    *(f4*)(act + i) = f4{v[0], v[1], v[2], v[3]};
+  } else {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    typedef float f2_ __attribute__((ext_vector_type(2)));
+    typedef __bf16 bh2_ __attribute__((ext_vector_type(2)));
+    auto pk2 = [](float a, float b) {
+      return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2_{a, b}, bh2_));
+    };
+    if constexpr (is_x3<T>) {
+      constexpr int PL = Cfg<T>::M * ROW;
+      float r1[8], r2[8];
+      u32x4 w0, w1, w2;
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const uint32_t h = pk2(v[e], v[e + 1]);
+        w0[e / 2] = h;
+        r1[e] = v[e] - __uint_as_float(h << 16);
+        r1[e + 1] = v[e + 1] - __uint_as_float(h & 0xffff0000u);
+        const uint32_t h1 = pk2(r1[e], r1[e + 1]);
+        w1[e / 2] = h1;
+        r2[e] = r1[e] - __uint_as_float(h1 << 16);
+        r2[e + 1] = r1[e + 1] - __uint_as_float(h1 & 0xffff0000u);
+        w2[e / 2] = pk2(r2[e], r2[e + 1]);
+      }
+      *(u32x4*)(act + i) = w0;
+      *(u32x4*)(act + PL + i) = w1;
+      *(u32x4*)(act + 2 * PL + i) = w2;
+    } else {
+      *(u32x4*)(act + i) = u32x4{pk2(v[0], v[1]), pk2(v[2], v[3]), pk2(v[4], v[5]), pk2(v[6], v[7])};
+    }
+  }
+}
 // one value in T's saved / gradient row representation
 template <typename T> __device__ __forceinline__ typename Cfg<T>::st_t to_st(float v) {
   if constexpr (sizeof(typename Cfg<T>::st_t) == 4) return v;
@@ -448,7 +496,12 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
                                          const typename Cfg<T>::lds_t* act, int kc0, int nkb, f4 (&acc)[NT][MT],
                                          int lane, const float* __restrict__ bias, ARing<T, NT>& R) {
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
-  const int g = lane >> 4, li = lane & 15;
+  // an opaque copy of the lane id: the per-K-block LDS fragment addresses (the row swizzle makes each one distinct)
+  // and weight pointers are then recomputed at every call instead of being hoisted out of the caller's layer loop,
+  // where they would hold ~16 VGPRs across every GEMM (spilled and reloaded in the 4-wave dX and the x3 dX)
+  int ln = lane;
+  asm volatile("" : "+v"(ln));
+  const int g = ln >> 4, li = ln & 15;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const f4 b0 = bias ? *(const f4*)(bias + nrow0 + 16 * nt + 4 * g) : f4{0.f, 0.f, 0.f, 0.f};
@@ -459,7 +512,7 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
   const typename Cfg<T>::w_t* wp[NT];
   constexpr int FRAG = 64 * EPC;
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) wp[nt] = W + ((size_t)((nrow0 >> 4) + nt) * (ldw / KB) * 64 + lane) * EPC;
+  for (int nt = 0; nt < NT; ++nt) wp[nt] = W + ((size_t)((nrow0 >> 4) + nt) * (ldw / KB) * 64 + ln) * EPC;
   if constexpr (is_x3<T>) {
     // x3: per K-block and (nt, mt) the six bf16 products w_i x a_j (i + j <= 2), smallest first, each term issued
     // across all accumulators before the next so consecutive MFMAs never share one
@@ -1203,20 +1256,28 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
       for (int r = 0; r < 4; ++r)
         cw[t][r] = masks[lay.L * trunk_mask_words<T>(Npad) + mask_index(Npad, 0, p / 16, TT * q + t) + r];
     // statically indexed (tile t, feature cl) loops keep the mask words in registers (a runtime index into cw
-    // would put it in scratch)
+    // would put it in scratch); the colour-output sum runs over j < cd with the reference's order, unrolled to CMAX
+    // with a predicate, and every 16-byte chunk of the row goes to LDS in one store
+    constexpr int EPC = Cfg<T>::EPC;
 #pragma unroll
     for (int t = 0; t < TT; ++t)
 #pragma unroll
-      for (int cl = 0; cl < 16; ++cl) {
-        const int c = CPT * q + 16 * t + cl;
-        float dc = 0.0f;
-        for (int j = 0; j < cd; ++j) dc += du[j] * wo[j * HC + c];
-        // feature cl within its 16-feature tile: ballot word cl & 3, bit 16 * (cl >> 2) + point
-        const bool on = (cw[t][cl & 3] >> (16 * (cl >> 2) + (mt_ & 15))) & 1ull;
-        float dz = on ? dc : 0.0f;
-        if constexpr ((YANERF_ABLATE & 64) != 0) dz = (float)c;
-        lds_put1<T>(act, mt_, c, dz);
-        if constexpr (!PM) grad[(GR.dzc + c) * ld + p] = to_st<T>(dz);
+      for (int c0 = 0; c0 < 16; c0 += EPC) {
+        float dz[EPC];
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          const int cl = c0 + e, c = CPT * q + 16 * t + cl;
+          float dc = 0.0f;
+#pragma unroll
+          for (int j = 0; j < CMAX; ++j)
+            if (j < cd) dc += du[j] * wo[j * HC + c];
+          // feature cl within its 16-feature tile: ballot word cl & 3, bit 16 * (cl >> 2) + point
+          const bool on = (cw[t][cl & 3] >> (16 * (cl >> 2) + (mt_ & 15))) & 1ull;
+          dz[e] = on ? dc : 0.0f;
+          if constexpr ((YANERF_ABLATE & 64) != 0) dz[e] = (float)c;
+          if constexpr (!PM) grad[(GR.dzc + c) * ld + p] = to_st<T>(dz[e]);
+        }
+        lds_put_chunk<T>(act, mt_, (CPT * q + 16 * t + c0) / EPC, dz);
       }
   }
   lds_barrier();
@@ -1245,10 +1306,13 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
     }
   }
   lds_barrier();
-  // ---- dH_{L-1} = Wint^T dY + w_d (x) dsigma ; dZ_{L-1} = dH * [H_{L-1} > 0]
-  for (int l = lay.L; l >= 1; --l) {
-    // l == L: the heads -> last trunk layer; else trunk layer l -> layer l-1
-    const typename Cfg<T>::w_t* A = (l == lay.L) ? Wt + lay.wintT_off : Wt + lay.wt_off[l];
+  // ---- dH_{L-1} = Wint^T dY + w_d (x) dsigma ; dZ_{L-1} = dH * [H_{L-1} > 0], then trunk layer l -> l-1.
+  // One step: the GEMM with the transposed weights (Wint^T from the heads, else layer l's), then the masked epilogue
+  // into dZ_{l-1}. The step from the heads (HEAD: adds the density-head term w_d * dsigma) is peeled off the loop, so
+  // the loop body keeps no per-point dsigma values live.
+  auto trunk_step = [&](auto head, int l) {
+    constexpr bool HEAD = decltype(head)::value;
+    const typename Cfg<T>::w_t* A = HEAD ? Wt + lay.wintT_off : Wt + lay.wt_off[l];
     const int hl = l - 1;  // layer whose output gradient we form
     uint64_t bits[MW];
 #pragma unroll
@@ -1256,21 +1320,21 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
       bits[w] = masks[((((int64_t)hl * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane];
     gemm_lds<T, NT, MT>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring);
     if (l - 1 >= 1) ring_fill<T, NT>(ring, Wt + lay.wt_off[l - 1], wpl, 256, nrow0, 256 / KB, lane);
-    if constexpr (PM && !(YANERF_ABLATE & 128)) {  // the GEMM's input: dY (l == L) or dZ_l
-      if (l == lay.L) copy_tile_pm<T, NTHR, 256>(act, 0, grad + GR.dyx * Npad + p0 * 256, tid);
+    if constexpr (PM && !(YANERF_ABLATE & 128)) {  // the GEMM's input: dY (from the heads) or dZ_l
+      if constexpr (HEAD) copy_tile_pm<T, NTHR, 256>(act, 0, grad + GR.dyx * Npad + p0 * 256, tid);
       else copy_tile_pm<T, NTHR, 256>(act, 0, grad + (GR.dz0 + 256LL * l) * Npad + p0 * 256, tid);
     }
     lds_barrier();
-    const float* wd = Wf + lay.wd_off;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int n = nrow0 + 16 * nt + 4 * g;
-      f4 wdv = (l == lay.L) ? *(const f4*)(wd + n) : f4{0.f, 0.f, 0.f, 0.f};
+      f4 wdv = f4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (HEAD) wdv = *(const f4*)(Wf + lay.wd_off + n);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int m = 16 * mt + li;
         f4 v = acc[nt][mt];
-        if (l == lay.L) {
+        if constexpr (HEAD) {
           const float gsm = (p0 + m < N) ? g_sigma[p0 + m] : 0.0f;
           v = v + wdv * gsm;
         }
@@ -1283,7 +1347,9 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
       }
     }
     lds_barrier();
-  }
+  };
+  trunk_step(std::integral_constant<bool, true>{}, lay.L);
+  for (int l = lay.L - 1; l >= 1; --l) trunk_step(std::integral_constant<bool, false>{}, l);
   if constexpr (PM && !(YANERF_ABLATE & 128)) copy_tile_pm<T, NTHR, 256>(act, 0, grad + GR.dz0 * Npad + p0 * 256, tid);
 }
 

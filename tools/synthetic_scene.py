@@ -32,13 +32,14 @@ BLOBS = [  # centre, radius, peak density, colour
 
 def field(x: torch.Tensor):
     """sigma [...] and rgb [..., 3] at points x [..., 3] (view independent)."""
-    sig = torch.zeros(x.shape[:-1], dtype=x.dtype, device=x.device)
-    col = torch.zeros(x.shape, dtype=x.dtype, device=x.device)
-    for c, r, a, rgb in BLOBS:
-        d2 = ((x - torch.tensor(c, dtype=x.dtype, device=x.device)) ** 2).sum(-1)
-        s = a * torch.exp(-d2 / (2 * r * r))
-        sig = sig + s
-        col = col + s[..., None] * torch.tensor(rgb, dtype=x.dtype, device=x.device)
+    centre = torch.tensor([b[0] for b in BLOBS], dtype=x.dtype, device=x.device)        # [B,3]
+    inv2r2 = torch.tensor([1.0 / (2 * b[1] * b[1]) for b in BLOBS], dtype=x.dtype, device=x.device)
+    peak = torch.tensor([b[2] for b in BLOBS], dtype=x.dtype, device=x.device)
+    rgb = torch.tensor([b[3] for b in BLOBS], dtype=x.dtype, device=x.device)           # [B,3]
+    d2 = ((x[..., None, :] - centre) ** 2).sum(-1)                                      # [...,B]
+    s = peak * torch.exp(-d2 * inv2r2)
+    sig = s.sum(-1)
+    col = s @ rgb
     return sig, col / sig.clamp_min(1e-12)[..., None]
 
 
@@ -73,14 +74,17 @@ def render_view(c2w_blender: np.ndarray, H: int, W: int, near=2.0, far=6.0, n=10
     rgb = torch.zeros(H, W, 3, dtype=torch.float64, device=device)
     acc = torch.zeros(H, W, dtype=torch.float64, device=device)
     trans = torch.ones(H, W, dtype=torch.float64, device=device)
-    delta = (t[1] - t[0]) * d.norm(dim=-1)
-    for k in range(n):
-        s, c = field(o + t[k] * d)
+    delta = ((t[1] - t[0]) * d.norm(dim=-1))[..., None]                                  # [H,W,1]
+    CH = 64  # samples per vectorised chunk; transmittance carried across chunks
+    for k0 in range(0, n, CH):
+        tk = t[k0:k0 + CH]
+        s, c = field(o[..., None, :] + tk[:, None] * d[..., None, :])                    # [H,W,CH], [H,W,CH,3]
         a = 1.0 - torch.exp(-s * delta)
-        w = a * trans
-        rgb += w[..., None] * c
-        acc += w
-        trans = trans * (1.0 - a)
+        tr = trans[..., None] * torch.cumprod(torch.cat([torch.ones_like(a[..., :1]), 1.0 - a[..., :-1]], -1), -1)
+        w = a * tr
+        rgb += (w[..., None] * c).sum(-2)
+        acc += w.sum(-1)
+        trans = tr[..., -1] * (1.0 - a[..., -1])
     return torch.cat([rgb, acc[..., None]], -1).clamp(0, 1).float().cpu().numpy()
 
 

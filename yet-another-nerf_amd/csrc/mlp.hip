@@ -1246,7 +1246,14 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
     }
   }
   {
-    const float* wo = Wf + lay.wo_off;
+    // the colour-output weights (cd x HC fp32, <= 2 KB) are staged once in the LDS tile's PE columns, which the dX
+    // kernel never uses: the colour-head backward then reads them as 16-byte LDS broadcasts (the lanes of one point
+    // group read the same address) instead of CMAX * CPT per-lane global loads (measured: the colour head cost
+    // 0.16 ms of the 1.28 ms bf16 dX with those loads)
+    constexpr int WFPR = KPE * (int)sizeof(LT) / 4;  // fp32 slots per row in the PE columns
+    static_assert(WFPR % 8 == 0 && (CMAX * HC) / WFPR <= M, "colour-output weights in the PE columns");
+    auto wo_row = [&](int i) -> float* { return (float*)(act + (i / WFPR) * ROW + PE_COL) + (i % WFPR); };
+    for (int i = tid; i < CMAX * HC; i += NTHR) *wo_row(i) = i < cd * HC ? Wf[lay.wo_off + i] : 0.0f;
     // colour-hidden ReLU masks for this point: feature tiles CPT/16 * q .. (slot L)
     constexpr int TT = CPT / 16;
     uint64_t cw[TT][4];
@@ -1259,21 +1266,35 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
     // would put it in scratch); the colour-output sum runs over j < cd with the reference's order, unrolled to CMAX
     // with a predicate, and every 16-byte chunk of the row goes to LDS in one store
     constexpr int EPC = Cfg<T>::EPC;
+    lds_barrier();
 #pragma unroll
     for (int t = 0; t < TT; ++t)
 #pragma unroll
       for (int c0 = 0; c0 < 16; c0 += EPC) {
+        // dc[e] = sum_j du_j * Wo[j][c0 + e] over this chunk's EPC columns, j ascending (the reference's order);
+        // Wo's chunk row j is EPC consecutive slots of one LDS row
+        float dc[EPC];
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) dc[e] = 0.0f;
+#pragma unroll
+        for (int j = 0; j < CMAX; ++j)
+          if (j < cd) {
+#pragma unroll
+            for (int e = 0; e < EPC; e += 4) {
+              const f4 v = *(const f4*)wo_row(j * HC + CPT * q + 16 * t + c0 + e);
+              dc[e] += du[j] * v.x;
+              dc[e + 1] += du[j] * v.y;
+              dc[e + 2] += du[j] * v.z;
+              dc[e + 3] += du[j] * v.w;
+            }
+          }
         float dz[EPC];
 #pragma unroll
         for (int e = 0; e < EPC; ++e) {
           const int cl = c0 + e, c = CPT * q + 16 * t + cl;
-          float dc = 0.0f;
-#pragma unroll
-          for (int j = 0; j < CMAX; ++j)
-            if (j < cd) dc += du[j] * wo[j * HC + c];
           // feature cl within its 16-feature tile: ballot word cl & 3, bit 16 * (cl >> 2) + point
           const bool on = (cw[t][cl & 3] >> (16 * (cl >> 2) + (mt_ & 15))) & 1ull;
-          dz[e] = on ? dc : 0.0f;
+          dz[e] = on ? dc[e] : 0.0f;
           if constexpr ((YANERF_ABLATE & 64) != 0) dz[e] = (float)c;
           if constexpr (!PM) grad[(GR.dzc + c) * ld + p] = to_st<T>(dz[e]);
         }

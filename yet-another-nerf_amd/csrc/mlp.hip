@@ -1444,7 +1444,10 @@ template <> __device__ __forceinline__ float hsum16<bf16_t>(f4 v) {
 constexpr int DW_CPR = YANERF_DW_CPR;      // 16-byte chunks per staged row (4: one K-block, 8: two)
 constexpr int DW_RB = 16 * DW_CPR;          // staged row bytes
 constexpr int DW_RPI = 64 / DW_CPR;         // rows per DMA wave-instruction
-constexpr int DW_STAGES = DW_CPR == 4 ? 4 : 2, DW_STAGE_BYTES = 512 * DW_RB;
+#ifndef YANERF_DW_STAGES
+#define YANERF_DW_STAGES (YANERF_DW_CPR == 4 ? 4 : 2)
+#endif
+constexpr int DW_STAGES = YANERF_DW_STAGES, DW_STAGE_BYTES = 512 * DW_RB;
 // points per dW stage: one K-block of the dW MFMA per staged row (x3: always one bf16 K-block, register staged)
 constexpr int X3_SPTS = 32;
 static int64_t dw_stage_pts(int prec) {
@@ -1606,6 +1609,10 @@ __device__ __forceinline__ int pm_swz(int r) {
   else return 2 * ((r & 3) | (((r >> 3) & 1) << 2));
 }
 constexpr int PM_SPTS = 32;  // points per dW stage
+#ifndef YANERF_PM_STAGES
+#define YANERF_PM_STAGES 4
+#endif
+constexpr int PM_STAGES = YANERF_PM_STAGES;  // LDS-DMA ring depth of the point-major (bf16) dW tile
 typedef short s4v __attribute__((ext_vector_type(4)));
 // fragment of 16 features x 8 points (points 8g..8g+7 of the stage for lane group g) from an image with ROWB-byte rows
 template <int ROWB>
@@ -1667,7 +1674,7 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
     }
   }
   auto issue = [&](int64_t st) {
-    char* dst = smem + (int)(st % DW_STAGES) * DW_STAGE_BYTES;
+    char* dst = smem + (int)(st % PM_STAGES) * DW_STAGE_BYTES;
 #pragma unroll
     for (int i = 0; i < PW; ++i)
       __builtin_amdgcn_global_load_lds(src[i] + st * adv[i],
@@ -1685,18 +1692,19 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
     for (int q = 0; q < KTW; ++q) acc[nt][q] = zero;
   }
 #pragma unroll
-  for (int i = 0; i < DW_STAGES - 1; ++i)
+  for (int i = 0; i < PM_STAGES - 1; ++i)
     if (st_lo + i < st_hi) issue(st_lo + i);
   for (int64_t st = st_lo; st < st_hi; ++st) {
     const int64_t ahead = st_hi - 1 - st;
-    static_assert(DW_STAGES == 4, "wait ladder below");
-    if (ahead >= DW_STAGES - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (DW_STAGES - 2)) : "memory");
+    static_assert(PM_STAGES >= 3 && PM_STAGES <= 5, "wait ladder below");
+    if (ahead >= PM_STAGES - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (PM_STAGES - 2)) : "memory");
+    else if (PM_STAGES == 5 && ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * 2) : "memory");
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (st + DW_STAGES - 1 < st_hi) issue(st + DW_STAGES - 1);
-    const char* buf = smem + (int)(st % DW_STAGES) * DW_STAGE_BYTES;
+    if (st + PM_STAGES - 1 < st_hi) issue(st + PM_STAGES - 1);
+    const char* buf = smem + (int)(st % PM_STAGES) * DW_STAGE_BYTES;
     if (mma_wave) {
       f4 a[4];
 #pragma unroll
@@ -1883,7 +1891,7 @@ __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S,
 template <typename T>
 __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t Npad, int S, float* __restrict__ slab) {
   // x3: two buffers of three 384-row bf16 planes (144 KB); otherwise the LDS-DMA ring
-  __shared__ __attribute__((aligned(16))) char smem[is_x3<T> ? 2 * 3 * 384 * 64 : DW_STAGES * DW_STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[is_x3<T> ? 2 * 3 * 384 * 64 : (Cfg<T>::PM ? PM_STAGES : DW_STAGES) * DW_STAGE_BYTES];
   // 1-D grid in job order (heaviest first); inside a job, split-major so the k-tiles sharing a dZ slab run together
   const int b = blockIdx.x;
   int ji = 0;

@@ -107,6 +107,14 @@ int yanerf_mlp_backward(const yanerf_mlp_desc* d, int precision, const void* pac
                         const float* rgb, const float* g_sigma, const float* g_rgb, int64_t R, int64_t P,
                         float* const* grads, void* workspace, void* stream);
 
+/* yanerf_mlp_backward in two halves, so that a caller can order the two passes' halves across streams:
+ * phase 1 = the input-side walk (every layer's pre-activation gradient into `workspace`), phase 2 = the weight and
+ * bias gradients from those (into `grads`), 3 = both (= yanerf_mlp_backward). Phase 2 must follow phase 1 of the
+ * same call arguments, stream-ordered; `saved` and `workspace` must be unchanged in between. */
+int yanerf_mlp_backward_phase(const yanerf_mlp_desc* d, int precision, const void* packed, const void* saved,
+                              const float* rgb, const float* g_sigma, const float* g_rgb, int64_t R, int64_t P,
+                              float* const* grads, void* workspace, int phase, void* stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Emission-absorption compositing (EmissionAbsorptionRaymarcher.forward,
  * yanerf/pipelines/renderers/multipass_emission_absorpsion_renderer.py:154-239).

@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""A/B of the fused training step with and without the side-stream overlap of the two MLP backwards (Lego config,
+"""A/B/C of the fused training step: serial, the whole coarse MLP backward on a side stream, or only its dW there (Lego config,
 4096 rays, 64 + 128), interleaved in one process, per precision. Development tool; prints one JSON line."""
 import json
 import math
@@ -25,7 +25,7 @@ def main(steps=20, rounds=3):
     focal = torch.tensor([0.5 * 800 / math.tan(0.5 * 0.6911112)], device=dev)
     res = {}
     for prec in (sys.argv[1].split(",") if len(sys.argv) > 1 else ("fp32", "bf16", "fp32x3")):
-        trs = {ov: NeRFTrainer(cfg.pipeline, precision=prec, device=dev, overlap=ov) for ov in (False, True)}
+        trs = {ov: NeRFTrainer(cfg.pipeline, precision=prec, device=dev, overlap=ov) for ov in (False, "both", "split")}
         best = {ov: float("inf") for ov in trs}
         for r in range(rounds):
             for ov, tr in trs.items():
@@ -37,7 +37,8 @@ def main(steps=20, rounds=3):
                     tr.step(poses[i % len(poses)][None], focal, image)
                 torch.cuda.synchronize()
                 best[ov] = min(best[ov], (time.perf_counter() - t0) / steps * 1e3)
-        res[prec] = {"ms_serial": round(best[False], 3), "ms_overlap": round(best[True], 3)}
+        res[prec] = {"ms_serial": round(best[False], 3), "ms_overlap": round(best["both"], 3),
+                     "ms_split": round(best["split"], 3)}
         del trs
     print(json.dumps(res))
 

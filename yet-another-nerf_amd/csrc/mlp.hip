@@ -2125,7 +2125,8 @@ static int launch_fwd(const MlpLayout& L, int prec, const void* packed, const fl
 
 template <typename T>
 static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const void* saved, const float* rgb,
-                      const float* gs, const float* gr, int64_t N, float* const* grads, void* ws, hipStream_t st) {
+                      const float* gs, const float* gr, int64_t N, float* const* grads, void* ws, hipStream_t st,
+                      int phase) {
   typedef typename Cfg<T>::st_t ST;
   const int64_t Npad = npad_of(prec, N);
   const typename Cfg<T>::w_t* Wt = (const typename Cfg<T>::w_t*)packed;
@@ -2135,9 +2136,12 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   int64_t grad_bytes = GR.rows * (Cfg<T>::PM ? Npad : row_ld(Npad, sizeof(ST))) * (int64_t)sizeof(ST);
   float* slab = (float*)((char*)ws + grad_bytes);
   const uint64_t* masks = (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM));
-  hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::DXWAVES * 64), 0, st, L, Wt,
-                     Wf, masks, rgb, gs, gr, N, Npad, gradbuf);
-  YN_LAUNCH_CHECK("mlp_backward_dx");
+  if (phase & 1) {
+    hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::DXWAVES * 64), 0, st, L,
+                       Wt, Wf, masks, rgb, gs, gr, N, Npad, gradbuf);
+    YN_LAUNCH_CHECK("mlp_backward_dx");
+  }
+  if (!(phase & 2)) return 0;
   DwJobs D;
   build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D);
   const int S = dw_splits(D.total_tiles, Npad / dw_stage_pts(prec));
@@ -2229,20 +2233,28 @@ int yanerf_mlp_forward(const yanerf_mlp_desc* d, int precision, const void* pack
 int yanerf_mlp_backward(const yanerf_mlp_desc* d, int precision, const void* packed, const void* saved,
                         const float* rgb, const float* g_sigma, const float* g_rgb, int64_t R, int64_t P,
                         float* const* grads, void* workspace, void* stream) {
+  return yanerf_mlp_backward_phase(d, precision, packed, saved, rgb, g_sigma, g_rgb, R, P, grads, workspace, 3,
+                                   stream);
+}
+
+int yanerf_mlp_backward_phase(const yanerf_mlp_desc* d, int precision, const void* packed, const void* saved,
+                              const float* rgb, const float* g_sigma, const float* g_rgb, int64_t R, int64_t P,
+                              float* const* grads, void* workspace, int phase, void* stream) {
   if (check_desc(d)) return 1;
+  YN_CHECK(phase >= 1 && phase <= 3, "mlp_backward: bad phase %d", phase);
   YN_CHECK(packed && saved && rgb && g_sigma && g_rgb && grads && workspace, "mlp_backward: null pointer");
   for (int i = 0; i < num_params(d); ++i) YN_CHECK(grads[i], "mlp_backward: grad %d is null", i);
   if (R * P == 0) return 0;
   MlpLayout L = make_layout(d, precision);
   if (precision == YANERF_PREC_F32)
     return launch_bwd<float>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R * P, grads, workspace,
-                             as_stream(stream));
+                             as_stream(stream), phase);
   if (precision == YANERF_PREC_BF16)
     return launch_bwd<bf16_t>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R * P, grads, workspace,
-                              as_stream(stream));
+                              as_stream(stream), phase);
   if (precision == YANERF_PREC_F32X3)
     return launch_bwd<x3_t>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R * P, grads, workspace,
-                            as_stream(stream));
+                            as_stream(stream), phase);
   YN_CHECK(false, "mlp_backward: bad precision %d", precision);
 }
 

@@ -116,8 +116,12 @@ class NeRFTrainer:
         self.ws = [torch.empty(p.ws_bytes, dtype=torch.uint8, device=self.dev) for p in self.passes]
         # measured (tools/ab_overlap.py, step ms serial -> overlapped): fp32 31.45 -> 31.22, bf16 5.53 -> 5.44,
         # fp32x3 20.17 -> 20.36 (its dW holds 144 KB of LDS per workgroup, so the two backwards only contend): off there
+        # overlap: False = serial, True / "both" = the whole coarse backward on the side stream beside the fine one,
+        # "split" = the coarse input-side walk (dX) first on the main stream, then its weight gradients (dW, a
+        # byte-bound kernel) on the side stream beside the fine dX (an MFMA-bound kernel)
         if overlap is None:
             overlap = precision != "fp32x3"
+        self.overlap = "both" if overlap is True else overlap
         self.side = torch.cuda.Stream(device=self.dev) if overlap else None
         self.grad_ptrs = [_C.ptr_array([p.grad.data_ptr() for p in ps]) for ps in self.params]
         self.param_ptrs = [_C.ptr_array([p.data_ptr() for p in ps]) for ps in self.params]
@@ -202,6 +206,13 @@ class NeRFTrainer:
         if self.side is None:
             self._mlp_backward(1, st)
             self._mlp_backward(0, st)
+        elif self.overlap == "split":
+            self._mlp_backward(0, st, phase=1)
+            self.side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.side):
+                self._mlp_backward(0, ctypes.c_void_p(self.side.cuda_stream), self.side, phase=2)
+            self._mlp_backward(1, st)
+            torch.cuda.current_stream().wait_stream(self.side)
         else:
             # the two MLP backwards are independent: the coarse one runs on the side stream beside the fine one (the
             # overlap fills each kernel's tail wave and the gaps between the dX / dW / reduce launches); the forward
@@ -218,12 +229,13 @@ class NeRFTrainer:
                                float(self.eps), float(self.weight_decay), self.step_count, st), "yanerf_adam")
         return out
 
-    def _mlp_backward(self, k: int, st, stream=None):
+    def _mlp_backward(self, k: int, st, stream=None, phase: int = 3):
         L = _C.lib()
         ps, spec = self.passes[k], self.specs[k]
-        self._probe(f"mlp_bwd_{k}", lambda: _C.check(L.yanerf_mlp_backward(
+        name = f"mlp_bwd_{k}" if phase == 3 else f"mlp_bwd{phase}_{k}"
+        self._probe(name, lambda: _C.check(L.yanerf_mlp_backward_phase(
             ctypes.byref(ps.desc), spec.precision, _p(self.packed[k]), _p(ps.saved), _p(ps.rgb), _p(ps.g_sigma),
-            _p(ps.g_rgb), self.R, ps.P, self.grad_ptrs[k], _p(self.ws[k]), st), "yanerf_mlp_backward"), stream)
+            _p(ps.g_rgb), self.R, ps.P, self.grad_ptrs[k], _p(self.ws[k]), phase, st), "yanerf_mlp_backward"), stream)
 
     # --------------------------------------------------------------------------------------- evaluation
     def _eval_buffers(self, R: int) -> Dict[str, torch.Tensor]:

@@ -105,7 +105,7 @@ def cpu_baseline(precision_cfg, n_pts_c: int, n_pts_f_new: int, budget_s: float 
                       f"in batches of {R}, numpy fp32 oracle, {dt:.1f} s"}
 
 
-def extras(pcfg, cfg, dev, poses, focal, image, precision):
+def extras(pcfg, cfg, dev, poses, focal, image, precision, others=()):
     """Secondary timings (not the headline): (1) full 800x800 evaluation render through the registry
     NeRFPipeline (no_grad, the reference's 131072-point chunking), (2) one training step through the drop-in
     path: registry NeRFPipeline + torch autograd + torch.optim.Adam, i.e. what scripts/run.py would run."""
@@ -142,6 +142,28 @@ def extras(pcfg, cfg, dev, poses, focal, image, precision):
     out["eval_render_fused"] = {"rays_per_s": round(H * W / dt, 1), "s_per_image": round(dt, 3),
                                 "chunk_rays": 65536, "precision": precision}
     del tr
+    # the fused evaluation render in every precision mode, with its whole-image MFMA utilisation (inference FLOPs:
+    # 2 x (589,952 MAC/point x (Pc + Pc + Pf) points + 3,456 MAC/ray/pass x 2) per ray)
+    Pc = int(pcfg.ray_sampler.n_pts_per_ray_evaluation)
+    Pn = int(pcfg.renderer.n_pts_per_ray_fine_evaluation)
+    inf_flops_ray = 2.0 * (MAC_PER_POINT * (Pc + Pc + Pn) + 2 * MAC_PER_RAY_PASS)
+    out["eval_render_fused_by_precision"] = {}
+    for p in (precision,) + tuple(others):
+        tr = NeRFTrainer(pcfg, precision=p, device=dev, n_rays=256)
+        tr.render(poses[:1], focal, 64, 64)
+        torch.cuda.synchronize()
+        best = float("inf")
+        for rep in range(2):
+            t0 = time.perf_counter()
+            tr.render(poses[2 + rep:3 + rep], focal, H, W)
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        rps = H * W / best
+        out["eval_render_fused_by_precision"][p] = {
+            "rays_per_s": round(rps, 1), "s_per_image": round(best, 4),
+            "mfma_tflops": round(rps * inf_flops_ray / 1e12, 1),
+            "mfma_frac": round(rps * inf_flops_ray / 1e12 / PEAK_TFLOPS[p], 4)}
+        del tr
     pipe.train()
     opt = torch.optim.Adam(pipe.parameters(), lr=float(cfg.runner.init_lr))
     steps = 5
@@ -297,7 +319,7 @@ def main():
         }
         del tr2
     if not args.no_extras:
-        result["extras"] = extras(pcfg, cfg, dev, poses, focal, image, args.precision)
+        result["extras"] = extras(pcfg, cfg, dev, poses, focal, image, args.precision, tuple(sec))
     if rank == 0 and world == 1 and args.psnr_steps > 0:
         result["psnr"] = psnr_leg(args.precision, args.psnr_steps, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

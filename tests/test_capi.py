@@ -93,3 +93,18 @@ def test_argument_validation_returns_error_without_launch():
     assert L.yanerf_refine(None, None, 4, 2, 8, 1, None, 0, 0, 1, None, None) == 1
     assert L.yanerf_raygen(None, None, None, None, 1, 1, 1, 1, 1.0, 1.0, 0.0, 1.0, 4, 0, None, 0, 0, None, None, None,
                            None, None, None) == 1
+
+
+def test_mlp_backward_phase_validation():
+    """yanerf_mlp_backward_phase rejects a phase outside 1..3 and null buffers before any launch."""
+    L = _C.lib()
+    d = lego_desc()
+    dummy = ctypes.c_void_p(16)
+    grads = (ctypes.c_void_p * 32)(*([16] * 32))
+    args = [ctypes.byref(d), 0, dummy, dummy, dummy, dummy, dummy, 4, 64, grads, dummy]
+    assert L.yanerf_mlp_backward_phase(*args, 0, None) == 1
+    assert "phase 0" in L.yanerf_last_error().decode()
+    assert L.yanerf_mlp_backward_phase(*args, 4, None) == 1
+    args[2] = None
+    assert L.yanerf_mlp_backward_phase(*args, 1, None) == 1
+    assert "null" in L.yanerf_last_error().decode()

@@ -28,6 +28,9 @@
 // Development-only timing ablations (never set in the product build): 1 = no MFMA, 2 = no harmonic embedding,
 // 4 = no saved stores in the trunk epilogue, 8 = no VALU heads, 16 = no trunk LDS writes, 32 = no trunk barriers,
 // 64 = dX colour-head backward without its mask / weight math, 128 = dX without its point-major copies.
+#ifndef YANERF_F32_DB
+#define YANERF_F32_DB 0  // fp32 GEMM loop: double-buffered weight fragments (0: one set + copy, the earlier loop)
+#endif
 #ifndef YANERF_ABLATE
 #define YANERF_ABLATE 0
 #endif
@@ -669,6 +672,33 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
 #pragma unroll
     for (int r = 0; r < D - 1; ++r)
       if (kb + r < nkb) step(kb + r, a[r][0], false);
+    return;
+  }
+  if constexpr (YANERF_F32_DB) {
+    // fp32: the weight fragments are double-buffered in two static register sets (loop unrolled by two). Block
+    // kb+1's loads are issued before block kb's 64 MFMAs and pinned there by scheduling barriers, so each L2 round
+    // trip hides behind a whole K-block. (With one set and a copy, the compiler sank the loads to the end of the
+    // iteration and waited for them a few MFMAs later: an exposed L2 latency per K-block.)
+    f4 a0[NT], a1[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) a0[nt] = *(const f4*)(wp[nt]);
+    auto half = [&](int kb, const f4(&acur)[NT], f4(&anext)[NT]) {
+      const int kn = kb + 1 < nkb ? kb + 1 : kb;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) anext[nt] = *(const f4*)(wp[nt] + kn * FRAG);
+      if constexpr (YANERF_F32_DB == 1) __builtin_amdgcn_sched_barrier(0);
+      f4 b[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) b[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + kb * 4 + g);
+      mma_grid<T, NT, MT>(acur, b, acc);
+      if constexpr (YANERF_F32_DB == 1) __builtin_amdgcn_sched_barrier(0);
+    };
+    int kb = 0;
+    for (; kb + 2 <= nkb; kb += 2) {
+      half(kb, a0, a1);
+      half(kb + 1, a1, a0);
+    }
+    if (kb < nkb) half(kb, a0, a1);
     return;
   }
   f4 a[NT];
@@ -1444,6 +1474,10 @@ template <> __device__ __forceinline__ float hsum16<bf16_t>(f4 v) {
 constexpr int DW_CPR = YANERF_DW_CPR;      // 16-byte chunks per staged row (4: one K-block, 8: two)
 constexpr int DW_RB = 16 * DW_CPR;          // staged row bytes
 constexpr int DW_RPI = 64 / DW_CPR;         // rows per DMA wave-instruction
+#ifndef YANERF_DW_PF
+#define YANERF_DW_PF 0
+#endif
+constexpr bool DW_PF = YANERF_DW_PF;  // fp32 dW: prefetch the next stage's fragments during the current MFMAs
 #ifndef YANERF_DW_STAGES
 #define YANERF_DW_STAGES (YANERF_DW_CPR == 4 ? 4 : 2)
 #endif
@@ -1509,6 +1543,77 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
   for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
     for (int q = 0; q < KTW; ++q) acc[nt][q] = zero;
+  auto bias_rows = [&](const char* buf) {
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int idx = tid + DW_THREADS * i, row = idx / DW_CPR, ch = idx % DW_CPR;
+      if (row < BN) rsum[i] += hsum16<T>(*(const f4*)(buf + row * DW_RB + (ch << 4)));
+    }
+  };
+  if constexpr (DW_PF && KBS == 1) {
+    // Fragment prefetch: the wave reads stage st+1's MFMA fragments from LDS while it multiplies stage st's (held
+    // in registers since the previous iteration), so no stage starts on an LDS read latency. Stage st+1 must have
+    // landed at iteration st's barrier; the DMA issued after it (stage st + DW_STAGES - 1) fills buffer
+    // (st-1) % DW_STAGES, whose fragments were read at iteration st-2 and whose bias rows at iteration st-1.
+    static_assert(DW_STAGES >= 3, "prefetch ring");
+    constexpr int NB = KTW;
+    f4 a[2][4], b[2][NB];
+    auto read_frags = [&](const char* buf, f4 (&fa)[4], f4 (&fb)[NB]) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int row = wn * 64 + 16 * nt + li;
+        fa[nt] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, g) << 4));
+      }
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int row = BN + (wk * KTW + q) * 16 + li;
+        fb[q] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, g) << 4));
+      }
+    };
+    // wait until this wave's DMA of a stage has landed, given how many stages were issued after it
+    auto wait_dma = [&](int64_t after) {
+      if (after >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * 3) : "memory");
+      else if (after == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * 2) : "memory");
+      else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    auto mma = [&](const f4 (&fa)[4], const f4 (&fb)[NB]) {
+      if (!mma_wave) return;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int q = 0; q < NB; ++q)
+            acc[nt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[nt][ks], fb[q][ks], acc[nt][q], 0, 0, 0);
+    };
+    int64_t ihi = st_lo;  // next stage to issue
+#pragma unroll
+    for (int i = 0; i < DW_STAGES - 1; ++i)
+      if (ihi < st_hi) issue(ihi++);
+    if (st_lo < st_hi) {
+      wait_dma(ihi - 1 - st_lo);
+      __builtin_amdgcn_s_barrier();
+      if (mma_wave) read_frags(smem + (int)(st_lo % DW_STAGES) * DW_STAGE_BYTES, a[0], b[0]);
+    }
+    // two stages per trip so the fragment buffers alternate without register copies
+    for (int64_t st = st_lo; st < st_hi; st += 2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int64_t sc = st + h;
+        if (sc < st_hi) {
+          const bool has_next = sc + 1 < st_hi;
+          if (has_next) wait_dma(ihi - 1 - (sc + 1));
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          if (ihi < st_hi) issue(ihi++);
+          if (has_next && mma_wave) read_frags(smem + (int)((sc + 1) % DW_STAGES) * DW_STAGE_BYTES, a[h ^ 1], b[h ^ 1]);
+          mma(a[h], b[h]);
+          if (do_bias) bias_rows(smem + (int)(sc % DW_STAGES) * DW_STAGE_BYTES);
+        }
+      }
+    }
+  } else {
 #pragma unroll
   for (int i = 0; i < DW_STAGES - 1; ++i)
     if (st_lo + i < st_hi) issue(st_lo + i);
@@ -1559,13 +1664,8 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
         }
       }
     }
-    if (do_bias) {
-#pragma unroll
-      for (int i = 0; i < BPT; ++i) {
-        const int idx = tid + DW_THREADS * i, row = idx / DW_CPR, ch = idx % DW_CPR;
-        if (row < BN) rsum[i] += hsum16<T>(*(const f4*)(buf + row * DW_RB + (ch << 4)));
-      }
-    }
+    if (do_bias) bias_rows(buf);
+  }
   }
   float* out = slab + (int64_t)s * slab_elems + J.slab_off;
   const int kv = J.ktot + 1;

@@ -181,6 +181,32 @@ def extras(pcfg, cfg, dev, poses, focal, image, precision, others=()):
     R = int(c.ray_sampler.n_rays_per_image_sampled_from_mask)
     out["dropin_train"] = {"rays_per_s": round(R / dt, 1), "ms_per_step": round(1e3 * dt, 3), "precision": precision,
                            "path": "registry NeRFPipeline + autograd + torch.optim.Adam"}
+    # BASELINE configs[4] on one GPU: bf16, 64 coarse + 256 fine samples (64 + 320 = 384 points per ray), the same
+    # fused training step (4096 rays), with its whole-step MFMA utilisation and the fine forward's roofline
+    import copy as _copy
+    c4 = _copy.deepcopy(pcfg)
+    c4.renderer.n_pts_per_ray_fine_training = 256
+    c4.renderer.n_pts_per_ray_fine_evaluation = 256
+    tr = NeRFTrainer(c4, precision="bf16", device=dev)
+    for i in range(3):
+        tr.step(poses[i:i + 1], focal, image)
+    tr.enable_probes(["mlp_fwd_1"])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    steps4 = 10
+    for i in range(steps4):
+        tr.step(poses[(3 + i) % len(poses)][None], focal, image)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps4
+    R4, Pc4, Pf4 = tr.R, tr.Pc, tr.Pf
+    f4ms = tr.probe_ms().get("mlp_fwd_1", float("nan"))
+    fwd4 = 2.0 * (MAC_PER_POINT * R4 * Pf4 + MAC_PER_RAY_PASS * R4)
+    out["lego256_bf16_train"] = {
+        "config": "BASELINE configs[4] at 1 GPU: 64 coarse + 256 fine (64 + 320 fine-pass points), bf16",
+        "rays_per_s": round(R4 / dt, 1), "ms_per_step": round(1e3 * dt, 3), "pts_per_ray": Pc4 + Pf4,
+        "step_mfma_frac": round(train_flops_per_ray(Pc4, Pf4) * R4 / dt / 1e12 / PEAK_TFLOPS["bf16"], 4),
+        "fine_fwd_ms": round(f4ms, 4), "fine_fwd_mfma_frac": round(fwd4 / (f4ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"], 4)}
+    del tr
     return out
 
 

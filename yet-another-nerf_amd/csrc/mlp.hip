@@ -2100,10 +2100,13 @@ static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, const f
 }
 
 // point splits per dW tile: enough workgroups that the light jobs dispatched last fill the tail of the heavy ones
+#ifndef YANERF_DW_SMAX
+#define YANERF_DW_SMAX 64
+#endif
 static int dw_splits(int total_tiles, int64_t n_stages) {
-  int64_t S = (4096 + total_tiles - 1) / total_tiles;
+  int64_t S = (YANERF_DW_SMAX * 64 + total_tiles - 1) / total_tiles;
   if (S > n_stages) S = n_stages;
-  if (S > 64) S = 64;
+  if (S > YANERF_DW_SMAX) S = YANERF_DW_SMAX;
   if (S < 1) S = 1;
   return (int)S;
 }

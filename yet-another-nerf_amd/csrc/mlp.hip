@@ -31,6 +31,9 @@
 #ifndef YANERF_F32_DB
 #define YANERF_F32_DB 0  // fp32 GEMM loop: double-buffered weight fragments (0: one set + copy, the earlier loop)
 #endif
+#ifndef YANERF_PRIO
+#define YANERF_PRIO 0  // fp32 GEMM loop: 1 = raise the wave priority over its MFMA block (A/B variant)
+#endif
 #ifndef YANERF_ABLATE
 #define YANERF_ABLATE 0
 #endif
@@ -712,7 +715,9 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
     f4 b[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) b[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + kb * 4 + g);
+    if constexpr (YANERF_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     mma_grid<T, NT, MT>(a, b, acc);
+    if constexpr (YANERF_PRIO == 1) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) a[nt] = an[nt];
   }

@@ -64,6 +64,55 @@ def synthetic_pose(theta, phi, radius=4.0):
     return (c2w @ np.diag([1.0, -1.0, -1.0, 1.0]))[:3, :4].astype(np.float32)
 
 
+# algorithmic MACs per point of the input-gradient walk (mlp_bwd_dx_kernel): every layer's input gradient except layer
+# 0's (the embedding carries no gradient): trunk l1..l7 over their 256 hidden inputs, intermediate 256x256, density
+# 256, colour layer over its 256 feature inputs, output 3x128
+MAC_PER_POINT_DX = 8 * 256 * 256 + 256 + 128 * 256 + 3 * 128
+# HBM-bound kernel ceilings are not used here: the three MLP kernels are priced against the MFMA peak of their mode
+
+
+def kernel_flops(kind: str, R: int, P: int) -> float:
+    """Algorithmic FLOPs of one launch of an MLP kernel over R rays x P points."""
+    if kind == "dx":
+        return 2.0 * MAC_PER_POINT_DX * R * P
+    return 2.0 * (MAC_PER_POINT * R * P + MAC_PER_RAY_PASS * R)  # forward and weight gradients
+
+
+def kernel_rooflines(tr, poses, focal, image, precision: str, steps: int = 4):
+    """Per-kernel HIP-event timings of the fine pass's three MLP kernels (forward, dX walk, dW), each alone on the
+    stream: the trainer's probe mode serialises the backward (dX, dW, slab reduce per pass; coarse after fine), so no
+    kernel shares the GPU while it is timed. Returns {kernel: roofline dict} and the dominant kernel by time."""
+    tr.kernel_probes = True
+    names = ["mlp_fwd_1", "mlp_dx_1", "mlp_dw_1", "mlp_reduce_1", "mlp_fwd_0", "mlp_dx_0", "mlp_dw_0", "mlp_reduce_0"]
+    tr.enable_probes(names)
+    for i in range(steps):
+        tr.step(poses[i % len(poses)][None], focal, image)
+    torch.cuda.synchronize()
+    ms = tr.probe_ms()
+    tr.kernel_probes = False
+    tr.events = None
+    R, Pf = tr.R, tr.Pf
+    peak = PEAK_TFLOPS[precision]
+    out = {}
+    for kind, kname in (("fwd", "mlp_fwd_kernel"), ("dx", "mlp_bwd_dx_kernel"), ("dw", "mlp_dw_kernel")):
+        t_ms = ms.get(f"mlp_{kind}_1", float("nan"))
+        fl = kernel_flops(kind, R, Pf)
+        ach = fl / (t_ms * 1e-3) / 1e12
+        pmc = ROOT / "profiles" / f"pmc_mlp_{kind}_{precision}.json"
+        traffic = None
+        if pmc.exists():
+            try:
+                traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out[kind] = {"bound": "mfma", "kernel": f"{kname} (fine pass)", "achieved": round(ach, 2), "peak": peak,
+                     "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic, "flops_per_launch": fl,
+                     "avg_launch_ms": round(t_ms, 4)}
+    dom = max(out, key=lambda k: out[k]["avg_launch_ms"])
+    serial_ms = {k: round(v, 4) for k, v in ms.items()}
+    return out, dom, serial_ms
+
+
 def train_flops_per_ray(pc: int, pf: int) -> float:
     fwd = 2.0 * (MAC_PER_POINT * (pc + pf) + 2 * MAC_PER_RAY_PASS)
     return 3.0 * fwd  # forward + input-gradient chain + weight gradients
@@ -101,8 +150,18 @@ def cpu_baseline(precision_cfg, n_pts_c: int, n_pts_f_new: int, budget_s: float 
     if limiter is not None:
         limiter.unregister()
     return {"value": round(done / dt, 2), "unit": "rays/s", "cores": threads, "kind": "port",
+            "what": "oracle/nerf_oracle.py: this repo's numpy restatement of the reference's training step, NOT the "
+                    "reference itself (which cannot run on the GPU box)",
             "sample": f"{done} rays of the Lego 64+{n_pts_f_new} training step (fwd+bwd both MLPs, no optimizer) "
                       f"in batches of {R}, numpy fp32 oracle, {dt:.1f} s"}
+
+
+# The reference's own CPU path (scripts/run.py --device cpu, torch 2.10 CPU, Lego 64 + 128, 4096 rays), timed in the
+# build container on 8 Xeon cores: 330-390 train rays/s. It is not re-timed here (the
+# reference does not exist on the GPU box); stated beside the port so the ratio against the reference is visible.
+REFERENCE_CPU = {"value": 360.0, "range": [330.0, 390.0], "unit": "rays/s", "cores": 8, "kind": "reference",
+                 "where": "build container, SURVEY.md §6 (not the GPU box)",
+                 "sample": "reference scripts/run.py --device cpu training steps, Lego 64+128, 4096 rays"}
 
 
 def extras(pcfg, cfg, dev, poses, focal, image, precision, others=()):
@@ -260,12 +319,12 @@ def main():
     focal = torch.tensor([focal_px], device=dev)
 
     def run(precision: str, steps: int, warmup: int, probes: bool):
-        tr = NeRFTrainer(pcfg, precision=precision, device=dev, lr=float(cfg.runner.init_lr) * world,
-                         n_rays=args.rays)
+        # the reference runner's schedule (warm-up, exponential decay; init/min lr scaled by the world size)
+        tr = NeRFTrainer(pcfg, precision=precision, device=dev, runner_cfg=cfg.runner, n_rays=args.rays)
         for i in range(warmup):
             tr.step(poses[(i + rank) % len(poses)][None], focal, image)
-        if probes:
-            tr.enable_probes(["mlp_fwd_0", "mlp_fwd_1", "mlp_bwd_0", "mlp_bwd_1"])
+        if probes:  # HIP events around the two forward launches (they have the GPU to themselves)
+            tr.enable_probes(["mlp_fwd_0", "mlp_fwd_1"])
         parallel.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -285,18 +344,10 @@ def main():
     ms_step = 1e3 * dt / args.steps
     probe = tr.probe_ms()
     flops_ray = train_flops_per_ray(Pc, Pf)
-    # roofline of the dominant kernel: fine-pass fused PE+MLP+heads forward (one launch per step)
-    fwd_flops = 2.0 * (MAC_PER_POINT * R * Pf + MAC_PER_RAY_PASS * R)
-    fwd_ms = probe.get("mlp_fwd_1", float("nan"))
-    achieved = fwd_flops / (fwd_ms * 1e-3) / 1e12
+    # per-kernel rooflines of the fine pass (each kernel timed alone, after the timed region); `roofline` is the
+    # dominant kernel by time, the others are listed beside it
+    rk, dom, serial_ms = kernel_rooflines(tr, poses, focal, image, args.precision)
     peak = PEAK_TFLOPS[args.precision]
-    pmc_file = ROOT / "profiles" / f"pmc_mlp_fwd_{args.precision}.json"
-    traffic = None
-    if pmc_file.exists():
-        try:
-            traffic = json.loads(pmc_file.read_text()).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
     result = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -312,12 +363,12 @@ def main():
         "data": "synthetic (random 800x800 target per rank, 40 spherical poses; random-init Lego MLPs)",
         "config": {"workload": "lego_800x800_64c_128f_train_step", "rays_per_gpu": R, "pts_per_ray": Pc + Pf,
                    "global_batch_rays": R * world, "parallelism": f"dp{world}", "precision": args.precision},
-        "roofline": {"bound": "mfma", "kernel": "mlp_fwd_kernel (fine pass)", "achieved": round(achieved, 2),
-                     "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                     "flops_per_launch": fwd_flops, "avg_launch_ms": round(fwd_ms, 4)},
+        "roofline": rk[dom],
+        "roofline_kernels": rk,
         "step_mfma_tflops": round(flops_ray * value / world / 1e12, 2),
         "step_mfma_frac": round(flops_ray * value / world / 1e12 / peak, 4),
-        "phase_ms": {k: round(v, 4) for k, v in probe.items()},
+        "fwd_ms_in_timed_steps": {k: round(v, 4) for k, v in probe.items()},
+        "kernel_ms_serialised": serial_ms,
     }
     del tr
     # the other precision modes on the same workload, reported beside the headline (never in `value`)
@@ -330,17 +381,17 @@ def main():
         result["secondary"] = {}
     for p2name in sec:
         tr2, dt2, _ = run(p2name, args.steps, args.warmup, probes=True)
-        p2 = tr2.probe_ms()
         v2 = R * world * args.steps / dt2
-        f2 = p2.get("mlp_fwd_1", float("nan"))
-        ach2 = fwd_flops / (f2 * 1e-3) / 1e12
+        fwd2 = {k: round(v, 4) for k, v in tr2.probe_ms().items()}
+        rk2, dom2, serial2 = kernel_rooflines(tr2, poses, focal, image, p2name)
         result["secondary"][p2name] = {
             "value": round(v2, 1), "unit": "rays/s",
             "ms_per_step": round(1e3 * dt2 / args.steps, 3),
-            "roofline": {"achieved": round(ach2, 2), "peak": PEAK_TFLOPS[p2name],
-                         "frac": round(ach2 / PEAK_TFLOPS[p2name], 4), "avg_launch_ms": round(f2, 4)},
+            "roofline": rk2[dom2],
+            "roofline_kernels": rk2,
             "step_mfma_frac": round(flops_ray * v2 / world / 1e12 / PEAK_TFLOPS[p2name], 4),
-            "phase_ms": {k: round(v, 4) for k, v in p2.items()},
+            "fwd_ms_in_timed_steps": fwd2,
+            "kernel_ms_serialised": serial2,
             "note": notes[p2name],
         }
         del tr2
@@ -351,6 +402,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(pcfg, Pc, Pf - Pc)
         result["vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
+        result["reference_cpu"] = REFERENCE_CPU
+        result["vs_reference_cpu"] = round(value / REFERENCE_CPU["value"], 1)
     if rank == 0:
         print(json.dumps(result))
     parallel.barrier()

@@ -110,7 +110,9 @@ int yanerf_mlp_backward(const yanerf_mlp_desc* d, int precision, const void* pac
 /* yanerf_mlp_backward in two halves, so that a caller can order the two passes' halves across streams:
  * phase 1 = the input-side walk (every layer's pre-activation gradient into `workspace`), phase 2 = the weight and
  * bias gradients from those (into `grads`), 3 = both (= yanerf_mlp_backward). Phase 2 must follow phase 1 of the
- * same call arguments, stream-ordered; `saved` and `workspace` must be unchanged in between. */
+ * same call arguments, stream-ordered; `saved` and `workspace` must be unchanged in between. Phase 2 is itself two
+ * launches, available separately for timing: 4 = the split-K weight-gradient kernel (partial slabs in `workspace`),
+ * then 8 = the deterministic slab reduction into `grads` (4 followed by 8 == 2). */
 int yanerf_mlp_backward_phase(const yanerf_mlp_desc* d, int precision, const void* packed, const void* saved,
                               const float* rgb, const float* g_sigma, const float* g_rgb, int64_t R, int64_t P,
                               float* const* grads, void* workspace, int phase, void* stream);
@@ -172,9 +174,12 @@ int yanerf_rgb_loss(const float* pred, const float* image, const float* xys, int
                     int64_t H, int64_t W, int64_t C, float scale, float* sq_err_per_ray, float* g_pred,
                     void* stream);
 
-/* Fused Adam step over a flat fp32 parameter buffer (torch.optim.Adam semantics, run.py:158-160). */
-int yanerf_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
-                float beta1, float beta2, float eps, float weight_decay, int64_t step, void* stream);
+/* Fused Adam step over a flat fp32 parameter buffer: torch.optim.Adam (run.py:158-160) with torch's arithmetic, one
+ * element per lane. The scalars are doubles, as torch holds them in Python: bias corrections 1 - beta**step, the step
+ * size lr / bc1 and sqrt(bc2) are computed on the host in double and rounded to float once, as torch passes them to
+ * its kernels. `step` is the 1-based step count after this update (Adam's state["step"]). */
+int yanerf_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
+                double beta1, double beta2, double eps, double weight_decay, int64_t step, void* stream);
 
 #ifdef __cplusplus
 }

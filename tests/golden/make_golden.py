@@ -23,6 +23,7 @@ import sys
 import types
 import zlib
 from contextlib import contextmanager
+from functools import partial
 from pathlib import Path
 
 import numpy as np
@@ -391,8 +392,127 @@ def gen_pipeline_state(out):
     out["pipeline_state"] = d
 
 
+@contextmanager
+def pytest_raises_any():
+    try:
+        yield
+    except (AttributeError, NameError, UnboundLocalError):
+        return
+    raise AssertionError("expected the reference RaySampler to fail on a mask")
+
+
+def gen_raysampler_masked(out):
+    """Masked / probability-weighted training ray sampling (ray_sampler.py:82-96, 178-227, 317-358) and LLFF-style
+    per-image tensor depth bounds (:280-283): the multinomial weights the reference builds (captured as the inputs
+    of torch.multinomial), the pixels it drew, its jitter and the resulting rays.
+
+    The reference's RaySampler.forward cannot take a mask at all (ray_sampler.py:87-89 reads self.image_height, an
+    attribute it never sets: AttributeError; with an explicit size the local is unbound), so the masked cases call its
+    training _RaySampler directly with the mask resized as :90-96 intends (nearest, configured size)."""
+    g = torch.Generator().manual_seed(3)
+    base = dict(type="RaySampler", image_width=10, image_height=6, n_rays_per_image_sampled_from_mask=5,
+                min_depth=0.5, max_depth=2.0, scene_extent=0.0, n_pts_per_ray_training=7, n_pts_per_ray_evaluation=7,
+                stratified_point_sampling_training=True, stratified_point_sampling_evaluation=False)
+    B, H, W = 2, 6, 10
+    poses = torch.randn(B, 3, 4, generator=g)
+    focal = torch.tensor([9.0, 11.5])
+    mask = (torch.rand(B, 1, 3, 5, generator=g) > 0.4).float()  # nearest-resized to 6 x 10 by the sampler
+    spm = torch.rand(B, H, W, generator=g) * (torch.rand(B, H, W, generator=g) > 0.3).float()
+    spm4 = torch.rand(B, 2, H, W, generator=g)
+    sparse = torch.zeros(B, 1, H, W)
+    sparse[0, 0, 1, 2] = sparse[0, 0, 4, 7] = sparse[0, 0, 5, 9] = 1.0  # 3 pixels < 5 rays: with replacement
+    sparse[1] = 1.0
+    near = torch.tensor([[0.75], [1.25]])
+    far = torch.tensor([[3.0], [4.5]])
+    cases = {
+        "mask": (dict(), dict(mask=mask)),
+        "mask_prob": (dict(), dict(mask=mask, sampling_prob_mask=spm)),
+        "prob_only": (dict(), dict(sampling_prob_mask=spm)),
+        "mask_nrays_none": (dict(n_rays_per_image_sampled_from_mask=None), dict(mask=mask)),
+        "layered": (dict(), dict(sampling_prob_mask=spm4, n_rays_per_image=[3, 4])),
+        "fallback": (dict(), dict(mask=sparse)),
+        "bounds": (dict(), dict(min_depth=near, max_depth=far)),
+    }
+    d = dict(poses=np32(poses), focal=np32(focal), mask=np32(mask), spm=np32(spm), spm4=np32(spm4), sparse=np32(sparse),
+             near=np32(near), far=np32(far))
+    for tag, (over, kw) in cases.items():
+        rs = RAY_SAMPLERS.build(Config(dict(r=dict(base, **over))).r)
+        kw = dict(kw)
+        if "mask" in kw:
+            with pytest_raises_any():
+                rs(poses, focal, EvaluationMode.TRAINING, **kw)  # the reference's own entry point fails here
+            kw["mask"] = torch.nn.functional.interpolate(kw["mask"], size=[H, W], mode="nearest")[:, 0]
+            call = rs._raysamplers[EvaluationMode.TRAINING]
+        else:
+            call = partial(rs, evaluation_mode=EvaluationMode.TRAINING)
+        calls = []
+        orig = torch.multinomial
+
+        def mn(inp, num, replacement=False, **k):
+            r = orig(inp, num, replacement=replacement, **k)
+            calls.append((inp.detach().clone(), bool(replacement), r.clone()))
+            return r
+
+        torch.multinomial = mn
+        rec = Recorder()
+        torch.manual_seed(17)
+        try:
+            with rec.capture():
+                rb = call(poses, focal, **kw)
+        finally:
+            torch.multinomial = orig
+        d[f"{tag}:n_calls"] = np.int64(len(calls))
+        for i, (inp, repl, r) in enumerate(calls):
+            d[f"{tag}:w{i}"] = np32(inp)
+            d[f"{tag}:repl{i}"] = np.int64(repl)
+        d[f"{tag}:jitter_u"] = np32(rec.take("rand_like")[0])
+        for k, v in rb._asdict().items():
+            d[f"{tag}:{k}"] = np32(v)
+    out["raysampler_masked"] = d
+
+
+def gen_lr_schedule(out):
+    """The reference runner's per-iteration learning rate (runners/apis.py:66-68: the decay scheduler from
+    runners/utils.py:89-109, then warmup_lr_scheduler while passed_iter <= warmup_steps) on a torch Adam whose group
+    carries init_lr (create_param_groups, runners/utils.py:148-151), with scripts/run.py:152-156's linear scaling of
+    init_lr / min_lr by the world size, for the Lego runner config and variants."""
+    from yanerf.runners.utils import create_lr_scheduler, warmup_lr_scheduler
+    base = Config.fromfile(str(REF / "configs/nerf/lego.yml")).runner
+    its = np.unique(np.concatenate([np.arange(0, 1010), np.arange(1010, 260000, 997), [199999, 250000, 259999]]))
+    d = dict(iters=its.astype(np.int64))
+    variants = {
+        "lego_w1": (dict(), 1),
+        "lego_w8": (dict(), 8),
+        "cosine_w2": (dict(lr_decay_type="cosine"), 2),
+        "nowarm_w1": (dict(warmup_steps=0), 1),
+        "shortwarm_cos_w1": (dict(lr_decay_type="cosine", warmup_steps=7, warmup_lr=2e-4, lr_decay_iters=50,
+                                  num_iters=300), 1),
+    }
+    for tag, (over, world) in variants.items():
+        cfg = Config(dict(runner=dict(base))).runner
+        for k, v in over.items():
+            cfg[k] = v
+        if world > 1 and cfg.linear_scale:  # scripts/run.py:152-156
+            cfg.init_lr = cfg.init_lr * world
+            cfg.min_lr = cfg.min_lr * world
+        p = torch.nn.Parameter(torch.zeros(1))
+        opt = torch.optim.Adam([{"params": [p], "init_lr": cfg.init_lr}], lr=cfg.init_lr)
+        sched = create_lr_scheduler(opt, cfg)
+        lrs = []
+        for it in its.tolist():
+            sched(iter=it)
+            if cfg["warmup_steps"] > 0 and it <= cfg["warmup_steps"]:
+                warmup_lr_scheduler(opt, it, cfg["warmup_steps"], cfg["warmup_lr"])
+            lrs.append(opt.param_groups[0]["lr"])
+        d[f"{tag}:lr"] = np.array(lrs, np.float64)
+        d[f"{tag}:world"] = np.int64(world)
+        d[f"{tag}:cfg"] = np.array([f"{k}={v!r}" for k, v in over.items()])
+    out["lr_schedule"] = d
+
+
 GENERATORS = (gen_harmonic, gen_raysampler, gen_mlp, gen_raymarcher, gen_sample_pdf, gen_render_eval,
-              gen_train_step, gen_zero_outputer, gen_init_checksums, gen_pipeline_state)
+              gen_train_step, gen_zero_outputer, gen_init_checksums, gen_pipeline_state, gen_lr_schedule,
+              gen_raysampler_masked)
 
 
 def main():

@@ -47,7 +47,7 @@ def test_reference_runner_convergence(precision):
     import yanerf_boot  # noqa: F401
     from yanerf_amd.pipelines import PIPELINES
     from yanerf_amd.pipelines.utils import EvaluationMode
-    from yanerf_amd.train import lr_at
+    from yanerf_amd.lr_schedule import apply_schedule, create_lr_scheduler
     torch.manual_seed(0)
     np.random.seed(0)
     cfg = copy.deepcopy(SMALL_PIPELINE)
@@ -61,15 +61,16 @@ def test_reference_runner_convergence(precision):
     focal = torch.ones(B, device=DEV)
     img = (torch.randn(H, W, 3).abs() * 255).to(torch.uint8).float() / 255.0  # test_runner.py:72-75
     images = img[None].expand(B, -1, -1, -1).contiguous().to(DEV)
-    opt = torch.optim.Adam(pipe.parameters(), lr=RUNNER["init_lr"])
+    # one param group carrying init_lr, as the reference's create_param_groups builds it (runners/utils.py:148-151)
+    opt = torch.optim.Adam([{"params": pipe.parameters(), "init_lr": RUNNER["init_lr"]}], lr=RUNNER["init_lr"])
+    sched = create_lr_scheduler(opt, RUNNER)
     pipe.train()
     order = np.arange(B)
     it = 0
     while it < RUNNER["num_iters"]:  # batch 2, drop_last (runners/utils.py:129-131): one batch per epoch
         np.random.shuffle(order)
         idx = torch.as_tensor(order[:2], device=DEV)
-        for gr in opt.param_groups:
-            gr["lr"] = lr_at(RUNNER, it)
+        apply_schedule(opt, sched, RUNNER, it)  # runners/apis.py:66-68
         preds = pipe(poses=poses[idx], focal_lengths=focal[idx], image_rgb=images[idx],
                      evaluation_mode=EvaluationMode.TRAINING)
         opt.zero_grad(set_to_none=True)

@@ -98,3 +98,149 @@ def test_sharded_render_and_evaluate_two_ranks():
         assert torch.equal(f, f0) and torch.equal(c, c0) and torch.equal(d, d0)
         for k, v in ev0.items():
             assert np.float64(ev[k]) == np.float64(v), (k, ev[k], v)
+
+
+# ------------------------------------------------------------------------------------------- training exchange
+def _spawn(target, world, extra=()):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + tuple(extra)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    try:
+        deadline = time.monotonic() + 150
+        while len(res) < world and time.monotonic() < deadline:
+            try:
+                res.append(q.get(timeout=2))
+            except queue.Empty:
+                assert all(p.is_alive() or p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+        res.sort(key=lambda x: x[0])
+        assert len(res) == world
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return res
+
+
+def _init_worker(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "tests" / "golden")]
+    import yanerf_boot  # noqa: F401
+    from yanerf_amd import parallel
+    parallel.init_distributed(backend="gloo")
+    torch.cuda.set_device(0)
+
+
+def _trainer_worker(rank, world, port, q):
+    """Three fused training steps per rank on rank-specific images; records each step's local (pre-exchange)
+    gradient, the exchanged gradient, the parameters and the sampled pixels."""
+    _init_worker(rank, world, port)
+    from scene import synthetic_pose
+    from yanerf_amd import parallel
+    from yanerf_amd.train import NeRFTrainer
+    from yanerf_amd.utils.config import Config
+    import yanerf_boot
+    cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml"))
+    tr = NeRFTrainer(cfg.pipeline, precision="fp32", device="cuda:0", n_rays=256, runner_cfg=cfg.runner, seed=42)
+    local = []
+    orig = parallel.allreduce_mean_
+
+    def spy(flat):
+        local.append(flat.detach().cpu().clone())
+        return orig(flat)
+
+    parallel.allreduce_mean_ = spy
+    g = torch.Generator().manual_seed(100 + rank)
+    img = torch.rand(1, 800, 800, 3, generator=g).to("cuda:0")
+    out = []
+    for k in range(3):
+        pose = torch.from_numpy(synthetic_pose(20.0 * k + 90.0 * rank, -30.0, 4.0)).float()[None].to("cuda:0")
+        tr.step(pose, torch.tensor([1111.111], device="cuda:0"), img)
+        torch.cuda.synchronize()
+        out.append(dict(local=local[-1], reduced=tr.flat.grad.detach().cpu().clone(),
+                        params=tr.flat.data.detach().cpu().clone(), xys=tr.xys.detach().cpu().clone(), lr=tr.lr))
+    parallel.allreduce_mean_ = orig
+    q.put((rank, out))
+    parallel.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_trainer_gradient_exchange_two_ranks():
+    """configs[2]'s exchange on the fused path (scripts/run.py:162-166 DDP semantics): per step, the exchanged gradient
+    is the mean of the ranks' local gradients (bit for bit), the parameters stay identical on every rank, the ranks
+    sample different pixels (Philox keyed by seed + rank, run.py:70-71), and the learning rate is the linearly scaled
+    schedule (run.py:152-156)."""
+    from yanerf_amd.lr_schedule import lr_at
+    from yanerf_amd.utils.config import Config
+    import yanerf_boot
+    runner = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml")).runner
+    res = _spawn(_trainer_worker, 2)
+    (_, a), (_, b) = res
+    for k in range(3):
+        mean = (a[k]["local"] + b[k]["local"]) / 2
+        assert torch.equal(a[k]["reduced"], mean) and torch.equal(b[k]["reduced"], mean), k
+        assert not torch.equal(a[k]["local"], b[k]["local"])
+        assert torch.equal(a[k]["params"], b[k]["params"]), k
+        assert not torch.equal(a[k]["xys"], b[k]["xys"])
+        assert a[k]["lr"] == lr_at(runner, k, world_size=2) == b[k]["lr"]
+
+
+def _ddp_worker(rank, world, port, q, golden_dir):
+    """The drop-in path as scripts/run.py:162-166 runs it: the registry NeRFPipeline wrapped in
+    DistributedDataParallel(find_unused_parameters=True); one step on rank-specific data with injected draws, and the
+    same step without DDP for the local gradient."""
+    _init_worker(rank, world, port)
+    from yanerf_amd import ops
+    from yanerf_amd.pipelines import PIPELINES
+    from yanerf_amd.pipelines.utils import EvaluationMode
+    from yanerf_amd.utils.config import Config
+    import yanerf_boot
+    cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml")).pipeline
+    cfg.ray_sampler.n_rays_per_image_sampled_from_mask = 64
+    torch.manual_seed(42)  # the same initial weights on every rank (DDP also broadcasts rank 0's)
+    pipe = PIPELINES.build(cfg).to("cuda:0")
+    ddp = torch.nn.parallel.DistributedDataParallel(pipe, find_unused_parameters=True)
+    g = torch.Generator().manual_seed(10 + rank)
+    R, Pc, Pn = 64, 64, 128
+    draws = dict(pixel_ids=torch.randperm(800 * 800, generator=g)[:R][None].to("cuda:0"),
+                 jitter_u=torch.rand(1, R, Pc, generator=g).to("cuda:0"),
+                 noise=[torch.randn(R, Pc, generator=g).to("cuda:0"), torch.randn(R, Pc + Pn, generator=g).to("cuda:0")],
+                 pdf_u=torch.rand(R, Pn, generator=g).to("cuda:0"))
+    from scene import synthetic_pose
+    pose = torch.from_numpy(synthetic_pose(45.0 * rank, -30.0, 4.0)).float()[None].to("cuda:0")
+    focal = torch.tensor([1111.111], device="cuda:0")
+    img = torch.rand(1, 800, 800, 3, generator=g).to("cuda:0")
+    ddp.train()
+
+    def run(model):
+        model.zero_grad(set_to_none=True)
+        with ops.injected_randomness(**{k: (list(v) if isinstance(v, list) else v) for k, v in draws.items()}):
+            preds = model(poses=pose, focal_lengths=focal, image_rgb=img, evaluation_mode=EvaluationMode.TRAINING)
+        preds["objective"].mean().backward()
+        torch.cuda.synchronize()
+        return torch.cat([p.grad.detach().reshape(-1).cpu() if p.grad is not None else torch.zeros(p.numel())
+                          for p in pipe.parameters()])
+
+    reduced = run(ddp)
+    local = run(pipe)
+    q.put((rank, local, reduced))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_ddp_registry_pipeline_two_ranks():
+    res = _spawn(_ddp_worker, 2, extra=("",))
+    (_, la, ra), (_, lb, rb) = res
+    mean = (la + lb) / 2
+    assert not torch.equal(la, lb)
+    assert torch.equal(ra, rb)
+    np.testing.assert_allclose(ra.numpy(), mean.numpy(), rtol=0, atol=1e-7 * float(mean.abs().max()))

@@ -1,0 +1,329 @@
+"""Parity of the fused training / evaluation path (train.NeRFTrainer: the path bench.py times) against the reference.
+
+* NeRFTrainer.step replays the reference's own training step (tests/golden/train_step_lego.npz: 48 rays, its pixel
+  ids, stratified jitter, density noise and refinement uniforms injected) and must reproduce its objective, coarse
+  loss and every parameter gradient at the registry path's gates (test_gpu_parity.test_train_step_lego).
+* yanerf_adam against torch.optim.Adam (scripts/run.py:158-160) on the same flat gradients.
+* yanerf_rgb_loss against sample_grid + squared error (pipelines/utils.py:189-196, 272-296) and its autograd gradient.
+* NeRFTrainer.render against the reference's two-pass evaluation render (render_eval_lego.npz), and a full 800x800
+  Lego evaluation image (BASELINE configs[1]) against the CPU oracle on a strided subset of its rays, per stage.
+* The learning-rate schedule inside the fused step (runners/apis.py:66-68).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nerf_oracle as O
+from parity_gates import split_gate
+from weights import LEGO_ARCH, make_nerf_mlp_params
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def t(x, dtype=torch.float32):
+    return torch.as_tensor(np.asarray(x), dtype=dtype, device=DEV)
+
+
+def n(x):
+    return x.detach().float().cpu().numpy()
+
+
+def close_frac(a, b, tol, frac, hard):
+    err = np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64))
+    assert err.max() <= hard, f"max err {err.max():.3e} > {hard:.3e}"
+    assert (err <= tol).mean() >= frac, f"only {(err <= tol).mean():.4f} within {tol:.3e}"
+
+
+def lego_cfg():
+    import yanerf_boot
+    from yanerf_amd.utils.config import Config
+    return Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml"))
+
+
+def pipeline_state(seeds):
+    sd = {}
+    for i, s in enumerate(seeds):
+        for k, v in make_nerf_mlp_params(LEGO_ARCH, int(s)).items():
+            sd[f"implicit_functions.{i}._fn.{k}"] = torch.from_numpy(v)
+    return sd
+
+
+def make_trainer(precision, seeds, n_rays=256, **kw):
+    from yanerf_amd.train import NeRFTrainer
+    tr = NeRFTrainer(lego_cfg().pipeline, precision=precision, device=DEV, n_rays=n_rays, **kw)
+    tr.load_pipeline_state_dict(pipeline_state(seeds))
+    return tr
+
+
+# ------------------------------------------------------------------------------------------- training step
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3"])
+def test_trainer_step_matches_reference_step(golden, precision):
+    from yanerf_amd import ops
+    g = golden("train_step_lego")
+    R = int(g["n_rays"])
+    tr = make_trainer(precision, g["seeds"], n_rays=R)
+    img = torch.zeros(1, 800, 800, 3, device=DEV)
+    img.view(1, -1, 3)[0, torch.as_tensor(g["pixel_ids"][0], device=DEV)] = t(g["gt_rgb"])
+    with ops.injected_randomness(pixel_ids=t(g["pixel_ids"], torch.int64), jitter_u=t(g["jitter_u"]),
+                                 noise=[t(g["noise_coarse"]), t(g["noise_fine"])], pdf_u=t(g["pdf_u"])):
+        out = tr.step(t(g["pose"]), t(g["focal"]), img)
+    torch.cuda.synchronize()
+    # the injected pixel ids were used (the gathered targets are the golden's)
+    ids = (n(tr.xys)[:, 0] + 800 * n(tr.xys)[:, 1]).astype(np.int64)
+    np.testing.assert_array_equal(ids, g["pixel_ids"][0])
+    obj = (out["sq_fine"].sum() + out["sq_coarse"].sum()) / (R * 3)
+    np.testing.assert_allclose(float(obj), float(g["objective"][0]), atol=1e-6, rtol=1e-5)
+    np.testing.assert_allclose(float(out["sq_coarse"].sum() / (R * 3)), float(g["loss_prev_stage_rgb_mse"][0]),
+                               atol=1e-7, rtol=1e-5)
+    worst = 0.0
+    for i, m in enumerate(tr.models):
+        for name, p in m.named_parameters():
+            v = n(p.grad).astype(np.float64)
+            if f"grad{i}:{name}" in g:
+                ref = g[f"grad{i}:{name}"].astype(np.float64)
+                mx = np.abs(ref).max()
+                close_frac(v, ref, 5e-3 * mx, 0.98, 3e-2 * mx)
+                rel = np.linalg.norm(v - ref) / max(np.linalg.norm(ref), 1e-30)
+            else:
+                s, nn = g[f"gradsum{i}:{name}"]
+                np.testing.assert_allclose(np.linalg.norm(v), nn, rtol=1e-3)
+                idx, ref = g[f"gradidx{i}:{name}"], g[f"gradval{i}:{name}"].astype(np.float64)
+                mx = np.abs(ref).max()
+                close_frac(v.reshape(-1)[idx], ref, 5e-3 * mx, 0.98, 3e-2 * mx)
+                rel = np.linalg.norm(v.reshape(-1)[idx] - ref) / max(np.linalg.norm(ref), 1e-30)
+            worst = max(worst, rel)
+    print(f"{precision}: trainer step vs reference, worst per-tensor relative L2 of the gradients {worst:.2e}")
+    assert worst < 2e-2
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_trainer_step_matches_registry_step(golden, precision):
+    """The fused step and the drop-in registry path (NeRFPipeline + autograd) on the same injected draws: same kernels,
+    so the gradients agree to float round-off (the registry path is the one test_gpu_parity pins to the reference)."""
+    from yanerf_amd import ops
+    from yanerf_amd.pipelines import PIPELINES
+    from yanerf_amd.pipelines.utils import EvaluationMode
+    g = golden("train_step_lego")
+    R = int(g["n_rays"])
+    cfg = lego_cfg().pipeline
+    cfg.ray_sampler.n_rays_per_image_sampled_from_mask = R
+    cfg.model.precision = precision
+    pipe = PIPELINES.build(cfg).to(DEV)
+    pipe.load_state_dict(pipeline_state(g["seeds"]), strict=False)
+    tr = make_trainer(precision, g["seeds"], n_rays=R)
+    img = torch.zeros(1, 800, 800, 3, device=DEV)
+    img.view(1, -1, 3)[0, torch.as_tensor(g["pixel_ids"][0], device=DEV)] = t(g["gt_rgb"])
+    draws = dict(pixel_ids=t(g["pixel_ids"], torch.int64), jitter_u=t(g["jitter_u"]),
+                 noise=[t(g["noise_coarse"]), t(g["noise_fine"])], pdf_u=t(g["pdf_u"]))
+    pipe.train()
+    with ops.injected_randomness(**draws):
+        preds = pipe(poses=t(g["pose"]), focal_lengths=t(g["focal"]), image_rgb=img,
+                     evaluation_mode=EvaluationMode.TRAINING)
+    preds["objective"].mean().backward()
+    with ops.injected_randomness(**draws):
+        out = tr.step(t(g["pose"]), t(g["focal"]), img)
+    torch.cuda.synchronize()
+    obj = float((out["sq_fine"].sum() + out["sq_coarse"].sum()) / (R * 3))
+    np.testing.assert_allclose(obj, float(preds["objective"].item()), rtol=1e-6)
+    for i, (f, m) in enumerate(zip(pipe.implicit_functions, tr.models)):
+        for (name, pa), (_, pb) in zip(f._fn.named_parameters(), m.named_parameters()):
+            a, b = n(pa.grad).astype(np.float64), n(pb.grad).astype(np.float64)
+            tol = (1e-5 if precision == "fp32" else 1e-3) * max(np.abs(a).max(), 1e-30)
+            np.testing.assert_allclose(b, a, atol=tol, err_msg=f"model {i} {name}")
+
+
+def test_trainer_lr_schedule_and_adam_state():
+    """With the runner config the fused step uses the reference schedule at passed_iter = steps taken (decay, then
+    warm-up; apis.py:66-68), and the Adam step count advances as torch's state['step']."""
+    from scene import synthetic_pose
+    from yanerf_amd.lr_schedule import lr_at
+    from yanerf_amd.train import NeRFTrainer
+    cfg = lego_cfg()
+    tr = NeRFTrainer(cfg.pipeline, precision="fp32", device=DEV, n_rays=128, runner_cfg=cfg.runner, seed=3)
+    pose = t(synthetic_pose(10.0, -30.0, 4.0)[None])
+    focal = t([1111.111])
+    img = torch.rand(1, 800, 800, 3, device=DEV)
+    for k in range(3):
+        tr.step(pose, focal, img)
+        assert tr.step_count == k + 1
+        assert tr.lr == lr_at(cfg.runner, k), (tr.lr, lr_at(cfg.runner, k))
+    assert tr.lr == cfg.runner.warmup_lr + (cfg.runner.init_lr - cfg.runner.warmup_lr) * 2 / cfg.runner.warmup_steps
+    with pytest.raises(ValueError):
+        NeRFTrainer(cfg.pipeline, device=DEV, n_rays=16, runner_cfg=cfg.runner, lr=1e-3)
+
+
+def test_trainer_rejects_bad_inputs_and_unsupported_options():
+    from yanerf_amd.train import NeRFTrainer
+    cfg = lego_cfg()
+    tr = NeRFTrainer(cfg.pipeline, device=DEV, n_rays=16)
+    pose, focal = torch.eye(4, device=DEV)[None, :3], torch.tensor([1111.0], device=DEV)
+    with pytest.raises(ValueError):
+        tr.step(pose, focal, torch.rand(1, 800, 800, 4, device=DEV))  # wrong colour count
+    with pytest.raises(ValueError):
+        tr.step(pose, focal, torch.rand(1, 800, 800, 3, device=DEV, dtype=torch.float64))
+    with pytest.raises(ValueError):
+        tr.step(pose.cpu(), focal, torch.rand(1, 800, 800, 3, device=DEV))
+    for mutate in (lambda c: c.ray_sampler.__setitem__("scene_extent", 2.0),
+                   lambda c: c.__setitem__("loss_weights", {"loss_rgb_mse": 1.0, "loss_prev_stage_rgb_mse": 0.5})):
+        c = lego_cfg().pipeline
+        mutate(c)
+        with pytest.raises(NotImplementedError):
+            NeRFTrainer(c, device=DEV, n_rays=16)
+
+
+def test_trainer_leaves_global_rng_untouched():
+    from yanerf_amd.train import NeRFTrainer
+    torch.manual_seed(123)
+    a = torch.rand(3)
+    torch.manual_seed(123)
+    NeRFTrainer(lego_cfg().pipeline, device=DEV, n_rays=16, seed=7)
+    b = torch.rand(3)
+    assert torch.equal(a, b)
+
+
+# ------------------------------------------------------------------------------------------- Adam, loss
+@pytest.mark.parametrize("wd", [0.0, 0.01])
+def test_adam_matches_torch_adam(wd):
+    """yanerf_adam against torch.optim.Adam (default GPU implementation) over 3 steps on 1,191,688 parameters (both
+    Lego MLPs): every parameter and moment within 1 ulp, and reported bit-equal fraction."""
+    from yanerf_amd import ops
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    N = 1_191_688
+    p0 = torch.randn(N, device=DEV, generator=gen) * 0.05
+    p = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.Adam([p], lr=5e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=wd)
+    mine, m, v = p0.clone(), torch.zeros(N, device=DEV), torch.zeros(N, device=DEV)
+    for step in range(1, 4):
+        grad = torch.randn(N, device=DEV, generator=gen) * 1e-3
+        p.grad = grad.clone()
+        opt.step()
+        ops.adam_step(mine, grad, m, v, lr=5e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=wd, step=step)
+        torch.cuda.synchronize()
+        st = opt.state[p]
+        assert int(float(st["step"])) == step
+        for name, a, b in (("param", mine, p.detach()), ("exp_avg", m, st["exp_avg"]),
+                           ("exp_avg_sq", v, st["exp_avg_sq"])):
+            ia, ib = a.view(torch.int32).long(), b.view(torch.int32).long()
+            ulp = (ia - ib).abs().max().item()
+            eq = (ia == ib).float().mean().item()
+            print(f"adam wd={wd} step {step} {name}: bit-equal {eq:.6f}, max ulp {ulp}")
+            assert ulp <= 1, (name, step, ulp)
+        # continue both from torch's state so the per-step comparison is not compounded
+        mine.copy_(p.detach())
+        m.copy_(st["exp_avg"])
+        v.copy_(st["exp_avg_sq"])
+
+
+def test_rgb_loss_matches_sample_grid_mse():
+    """yanerf_rgb_loss (the fused step's loss) against the reference formulation: sample_grid gathers the target at
+    the integer xys (pipelines/utils.py:272-296), per-ray squared error, and autograd of scale * sum((pred - gt)^2)."""
+    from yanerf_amd import ops
+    from yanerf_amd.pipelines.utils import sample_grid
+    gen = torch.Generator(device=DEV).manual_seed(1)
+    B, H, W, C, R = 2, 9, 13, 3, 37
+    image = torch.rand(B, H, W, C, device=DEV, generator=gen)
+    xs = torch.randint(0, W, (B, R), device=DEV, generator=gen)
+    ys = torch.randint(0, H, (B, R), device=DEV, generator=gen)
+    xys = torch.stack([xs, ys], -1).float()
+    pred = torch.rand(B, R, C, device=DEV, generator=gen)
+    scale = 1.0 / (R * C)
+    sq, g = ops.rgb_loss(pred, image, xys, scale)
+    gt = sample_grid(image, xys.view(B, R, 1, 2)).reshape(B, R, C)
+    pr = pred.clone().requires_grad_(True)
+    loss = ((pr - gt) ** 2).sum() * scale
+    loss.backward()
+    ref_sq = ((pred - gt) ** 2).sum(-1)
+    np.testing.assert_allclose(n(sq), n(ref_sq), rtol=2e-7, atol=0)
+    assert torch.equal(g, pr.grad), (g - pr.grad).abs().max()
+    np.testing.assert_allclose(float(sq.sum() * scale), float(loss), rtol=1e-6)
+
+
+# ------------------------------------------------------------------------------------------- evaluation render
+def test_trainer_render_matches_reference_render(golden):
+    """NeRFTrainer.render (the fused evaluation path) against the reference's two-pass EVALUATION render
+    (render_eval_lego.npz: 16 x 16 override grid of the 800 x 800 Lego camera, seeds 11 / 12): coarse stage strict,
+    fine stage through the split gate (parity_gates: strict wherever the refined depths agree)."""
+    from yanerf_amd import ops
+    g = golden("render_eval_lego")
+    H, W = int(g["H"]), int(g["W"])
+    R = H * W
+    for precision in ("fp32", "fp32x3"):
+        tr = make_trainer(precision, g["seeds"])
+        f, c, d = tr.render(t(g["pose"]), t(g["focal"]), H, W, chunk=100)
+        np.testing.assert_allclose(n(c).reshape(R, 3), g["coarse_features"].reshape(R, 3), atol=1e-5, rtol=0)
+        # refined depths from our coarse weights vs from the reference's (the renderer's own intermediate)
+        zc = t(O.sample_rays_eval(g["pose"], g["focal"], 800, 800, 2.0, 6.0, 64, H=H, W=W)[2].reshape(R, 64))
+        rb_w = tr_coarse_weights(tr, g, H, W)
+        z_gpu = n(ops.refine(zc, rb_w, 128, det=True))
+        z_ref = n(ops.refine(zc, t(g["coarse_weights"]).reshape(R, -1), 128, det=True))
+        split_gate(n(f), g["fine_features"], z_gpu, z_ref, n(d), g["fine_depths"], tag=f"render_eval {precision}")
+
+
+def tr_coarse_weights(tr, g, H, W):
+    """The coarse-stage weights the fused render computes for the golden camera (same kernels: raygen, coarse MLP,
+    composite), read through the C ABI."""
+    import ctypes
+
+    from yanerf_amd import _C
+    from yanerf_amd import ops
+    L = _C.lib()
+    R = H * W
+    pose, focal = t(g["pose"]).reshape(1, 3, 4).contiguous(), t(g["focal"]).reshape(1)
+    o, d, z, _, _ = ops.raygen(pose, focal, n_pts=64, near=2.0, far=6.0, cfg_w=800, cfg_h=800,
+                               pixel_ids=torch.arange(R, device=DEV)[None], grid_hw=(H, W))
+    spec = tr.specs[0]
+    packed = ops.mlp_pack(spec, tr.params[0])
+    sigma = torch.empty(R * 64, device=DEV)
+    rgb = torch.empty(R * 64, 3, device=DEV)
+    _C.check(L.yanerf_mlp_forward(ctypes.byref(spec.desc()), spec.precision, ops._p(packed), ops._p(o), ops._p(d),
+                                  ops._p(z), R, 64, ops._p(sigma), ops._p(rgb), None, ops._stream()), "fwd")
+    _, _, _, w = ops.composite(tr.march, sigma.view(R, 64, 1), rgb.view(R, 64, 3), z.view(R, 64), d.view(R, 3))
+    return w.reshape(R, 64)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3"])
+def test_full_image_800_vs_oracle(precision):
+    """BASELINE configs[1] at full size: one whole 800 x 800 Lego evaluation image (64 + 128 samples, 640,000 rays)
+    through the fused path (NeRFTrainer.render) and through the drop-in registry pipeline (313 chunks of 131,072
+    points, as nerf_pipeline.py:217-236 chunks it). 2,048 rays on a stride across the image are rendered by the CPU
+    oracle; the coarse stage is held to 1e-5 (RGB) / 1e-4 (depth) and the fine stage to the split gate."""
+    from scene import synthetic_pose
+    from yanerf_amd import ops
+    from yanerf_amd.pipelines import PIPELINES
+    from yanerf_amd.pipelines.utils import EvaluationMode
+    seeds = (11, 12)
+    tr = make_trainer(precision, seeds)
+    pose_np = synthetic_pose(30.0, -30.0, 4.0)[None]
+    pose, focal = t(pose_np), t([1111.1111])
+    f, c, d = tr.render(pose, focal)
+    assert f.shape == (800, 800, 3) and torch.isfinite(f).all()
+    cfg = lego_cfg().pipeline
+    cfg.model.precision = precision
+    pipe = PIPELINES.build(cfg).to(DEV)
+    pipe.load_state_dict(pipeline_state(seeds), strict=False)
+    pipe.eval()
+    with torch.no_grad():
+        preds = pipe(poses=pose, focal_lengths=focal, evaluation_mode=EvaluationMode.EVALUATION)
+    full_reg = n(preds["rendered_images"]).reshape(-1, 3)
+    # the two HIP paths render the same image (same kernels, deterministic refinement)
+    np.testing.assert_allclose(full_reg, n(f).reshape(-1, 3), atol=1e-6, rtol=0)
+    S = 2048
+    idx = (np.arange(S) * (800 * 800 // S) + 157).astype(np.int64)
+    o, dd, z, _ = O.sample_rays_eval(pose_np, np.array([1111.1111], np.float32), 800, 800, 2.0, 6.0, 64)
+    o, dd, z = o.reshape(-1, 3)[idx], dd.reshape(-1, 3)[idx], z.reshape(-1, 64)[idx]
+    pc, pf = (make_nerf_mlp_params(LEGO_ARCH, s) for s in seeds)
+    ref = O.render_two_pass(pc, pf, O.MLPArch.from_dict(LEGO_ARCH),
+                            O.RenderCfg(raymarch=O.RaymarchOpts(background_density_bias=1e-6)), o, dd, z)
+    np.testing.assert_allclose(n(c).reshape(-1, 3)[idx], ref["coarse"][0], atol=1e-5, rtol=0)
+    # the subset's coarse weights on the GPU: the registry renderer on exactly those rays, whose fine output must be
+    # the full image's pixels (same kernels), then the refined depths from both sets of coarse weights
+    with torch.no_grad():
+        ro = pipe.renderer(t(o)[None], t(dd)[None], t(z)[None], torch.zeros(1, S, 2, device=DEV), bg_color=None,
+                           implicit_functions=pipe.implicit_functions, evaluation_mode=EvaluationMode.EVALUATION)
+    np.testing.assert_allclose(n(ro.features).reshape(S, 3), n(f).reshape(-1, 3)[idx], atol=1e-6, rtol=0)
+    np.testing.assert_allclose(n(ro.prev_stage.depths).reshape(S), ref["coarse"][1].reshape(S), atol=1e-4, rtol=0)
+    z_gpu = n(ops.refine(t(z), ro.prev_stage.aux["weights"].reshape(S, 64), 128, det=True))
+    split_gate(n(f).reshape(-1, 3)[idx], ref["fine"][0], z_gpu, ref["z_fine"], n(d).reshape(-1)[idx],
+               ref["fine"][1].reshape(-1), tag=f"800x800 {precision}")

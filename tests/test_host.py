@@ -160,3 +160,26 @@ def test_adam_state_flat_conversion():
         for key in ("exp_avg", "exp_avg_sq"):
             assert torch.equal(opt.state_dict()["state"][i][key], opt2.state_dict()["state"][i][key])
     assert opt2.state_dict()["param_groups"][0]["betas"] == (0.8, 0.99)
+
+
+@pytest.mark.parametrize("tag", ["mask", "mask_prob", "prob_only", "mask_nrays_none", "layered", "fallback"])
+def test_sampling_weights_match_reference(golden, tag):
+    """The multinomial weights of masked / probability-weighted sampling equal the ones the reference's _RaySampler
+    builds (ray_sampler.py:181-216; captured inputs of torch.multinomial in raysampler_masked.npz)."""
+    from yanerf_amd.pipelines.ray_samplers.ray_sampler import RaySampler
+    g = golden("raysampler_masked")
+    T = torch.from_numpy
+    kw = {"mask": (g["mask"], None, 5), "mask_prob": (g["mask"], g["spm"], 5), "prob_only": (None, g["spm"], 5),
+          "mask_nrays_none": (g["mask"], None, None), "layered": (None, g["spm4"], [3, 4]),
+          "fallback": (g["sparse"], None, 5)}[tag]
+    mask = None if kw[0] is None else torch.nn.functional.interpolate(T(kw[0]), size=[6, 10], mode="nearest")[:, 0]
+    num = kw[2]
+    if num is None:  # ray_sampler.py:173-175: sample as many rays as the smallest mask holds
+        num = int(mask.sum(dim=(1, 2)).min().int().item())
+        assert num == g["mask_nrays_none:xys"].shape[1]
+    w, num = RaySampler._sampling_weights(2, 6, 10, num, mask, None if kw[1] is None else T(kw[1]), "cpu")
+    if w.dim() == 3:
+        for layer in range(w.shape[1]):
+            np.testing.assert_array_equal(w[:, layer].numpy(), g[f"{tag}:w{layer}"])
+    else:
+        np.testing.assert_array_equal(w.numpy(), g[f"{tag}:w0"])

@@ -25,7 +25,7 @@ sys.path.insert(0, str(ROOT / "tools"))
 import yanerf_boot  # noqa: E402,F401
 from synthetic_scene import write_scene  # noqa: E402
 from yanerf_amd.datasets import BlenderDataset, DeviceImageSet  # noqa: E402
-from yanerf_amd.train import NeRFTrainer, lr_at  # noqa: E402
+from yanerf_amd.train import NeRFTrainer  # noqa: E402
 from yanerf_amd.utils.config import Config  # noqa: E402
 
 
@@ -38,7 +38,7 @@ def run(data_dir: Path, precision: str, steps: int, dev, n_rays=4096, log=None):
     runner = dict(cfg.runner)
     runner["warmup_steps"] = max(1, steps // 10)
     runner["lr_decay_iters"] = steps * 1.25  # reach ~0.16x the initial rate at the end, like lego.yml's 200k/250k
-    tr = NeRFTrainer(pcfg, precision=precision, device=dev, n_rays=n_rays, lr=float(runner["init_lr"]), seed=42)
+    tr = NeRFTrainer(pcfg, precision=precision, device=dev, n_rays=n_rays, runner_cfg=runner, seed=42)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     it = 0
@@ -47,7 +47,6 @@ def run(data_dir: Path, precision: str, steps: int, dev, n_rays=4096, log=None):
         for i in train.epoch_order(epoch, seed=42):
             if it >= steps:
                 break
-            tr.lr = lr_at(runner, it)
             pose, focal, img, _, _ = train.item(i)
             tr.step(pose, focal, img)
             it += 1

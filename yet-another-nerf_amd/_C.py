@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, Structure, c_char_p, c_float, c_int, c_int32, c_int64, c_uint32, c_uint64, c_void_p
+from ctypes import POINTER, Structure, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_uint32, c_uint64, c_void_p
 from pathlib import Path
 
 LIB_PATH = Path(os.environ.get("YANERF_HIP_LIB", Path(__file__).resolve().parent / "libyanerf_hip.so"))
@@ -81,7 +81,7 @@ def lib():
         "yanerf_sample_pdf": (c_int, [P, P, i64, i64, i64, c_int, P, c_uint64, c_uint64, P, P]),
         "yanerf_refine": (c_int, [P, P, i64, i64, i64, c_int, P, c_uint64, c_uint64, c_int, P, P]),
         "yanerf_rgb_loss": (c_int, [P, P, P, i64, i64, i64, i64, i64, c_float, P, P, P]),
-        "yanerf_adam": (c_int, [P, P, P, P, i64, c_float, c_float, c_float, c_float, c_float, i64, P]),
+        "yanerf_adam": (c_int, [P, P, P, P, i64, c_double, c_double, c_double, c_double, c_double, i64, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -65,8 +65,11 @@ def split_pipeline_state(sd: Dict[str, torch.Tensor], n_models: int = 2):
 
 
 def adam_state_from_flat(params, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, step: int, lr: float,
-                         betas, eps: float, weight_decay: float) -> Dict:
-    """torch.optim.Adam.state_dict() for `params` (in order) from flat moment buffers."""
+                         betas, eps: float, weight_decay: float, init_lr: Optional[float] = None) -> Dict:
+    """torch.optim.Adam.state_dict() for `params` (in order) from flat moment buffers. The param group carries the
+    reference's `init_lr` key (runners/utils.py:148-151), which its lr schedulers read every iteration (:65-86):
+    torch's Optimizer.load_state_dict replaces the whole group with the saved one, so without it a reference run
+    resumed from this checkpoint would fail on its first scheduler call."""
     state, off = {}, 0
     for i, p in enumerate(params):
         n = p.numel()
@@ -74,7 +77,8 @@ def adam_state_from_flat(params, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor
                     "exp_avg": exp_avg[off:off + n].view_as(p).detach().cpu().clone(),
                     "exp_avg_sq": exp_avg_sq[off:off + n].view_as(p).detach().cpu().clone()}
         off += n
-    group = {"lr": float(lr), "betas": tuple(float(b) for b in betas), "eps": float(eps),
+    group = {"lr": float(lr), "init_lr": float(lr if init_lr is None else init_lr),
+             "betas": tuple(float(b) for b in betas), "eps": float(eps),
              "weight_decay": float(weight_decay), "amsgrad": False, "maximize": False, "foreach": None,
              "capturable": False, "differentiable": False, "fused": None, "params": list(range(len(params)))}
     return {"state": state if step > 0 else {}, "param_groups": [group]}

@@ -2249,14 +2249,21 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
                        Wt, Wf, masks, rgb, gs, gr, N, Npad, gradbuf);
     YN_LAUNCH_CHECK("mlp_backward_dx");
   }
-  if (!(phase & 2)) return 0;
+  // phase 2 = dW + reduce; 4 = the dW kernel alone, 8 = the slab reduce alone (4 then 8 == 2: for timing probes)
+  const bool dw = (phase & 2) || (phase & 4), red = (phase & 2) || (phase & 8);
+  if (!dw && !red) return 0;
   DwJobs D;
   build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D);
   const int S = dw_splits(D.total_tiles, Npad / dw_stage_pts(prec));
-  hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)(D.total_tiles * S)), dim3(DW_THREADS), 0, st, D, Npad, S, slab);
-  YN_LAUNCH_CHECK("mlp_backward_dw");
-  hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((D.slab_elems + 255) / 256)), dim3(256), 0, st, D, S, slab);
-  YN_LAUNCH_CHECK("mlp_backward_reduce");
+  if (dw) {
+    hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)(D.total_tiles * S)), dim3(DW_THREADS), 0, st, D, Npad, S,
+                       slab);
+    YN_LAUNCH_CHECK("mlp_backward_dw");
+  }
+  if (red) {
+    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((D.slab_elems + 255) / 256)), dim3(256), 0, st, D, S, slab);
+    YN_LAUNCH_CHECK("mlp_backward_reduce");
+  }
   return 0;
 }
 
@@ -2349,7 +2356,7 @@ int yanerf_mlp_backward_phase(const yanerf_mlp_desc* d, int precision, const voi
                               const float* rgb, const float* g_sigma, const float* g_rgb, int64_t R, int64_t P,
                               float* const* grads, void* workspace, int phase, void* stream) {
   if (check_desc(d)) return 1;
-  YN_CHECK(phase >= 1 && phase <= 3, "mlp_backward: bad phase %d", phase);
+  YN_CHECK(phase == 1 || phase == 2 || phase == 3 || phase == 4 || phase == 8, "mlp_backward: bad phase %d", phase);
   YN_CHECK(packed && saved && rgb && g_sigma && g_rgb && grads && workspace, "mlp_backward: null pointer");
   for (int i = 0; i < num_params(d); ++i) YN_CHECK(grads[i], "mlp_backward: grad %d is null", i);
   if (R * P == 0) return 0;

@@ -4,6 +4,8 @@
 // Layout: one thread per ray for ray generation / loss; one wave64 per ray for every per-ray scan
 // (compositing cumsum, CDF, merge), lanes owning contiguous sample chunks so HBM rows [R][P] are read
 // coalesced. Built with -ffp-contract=off so the float op sequence matches the reference's aten ops.
+#include <cmath>
+
 #include "common.hpp"
 
 namespace yanerf {
@@ -511,19 +513,31 @@ __global__ void rgb_loss_kernel(const float* __restrict__ pred, const float* __r
   if (sq) sq[gid] = acc;
 }
 
+// torch.optim.Adam's per-element arithmetic (torch/optim/adam.py _multi_tensor_adam, the default on the GPU), op for
+// op: the scalars arrive already rounded to float from the host's double arithmetic, exactly as torch casts its
+// Python-float scalars; which of the multiply-adds torch's own kernels fuse is YANERF_ADAM_FMA (bit 0 weight decay
+// `grad + wd * p`, bit 1 lerp `m + w1 * (g - m)`, bit 2 addcmul `v*b2 + (w2 * g) * g`, bit 3 addcdiv
+// `p + (-step_size) * (m / denom)`), pinned by tools/adam_emulation_check.py on the GPU.
+#ifndef YANERF_ADAM_FMA
+#define YANERF_ADAM_FMA 15
+#endif
+__device__ __forceinline__ float madd(bool fused, float a, float b, float c) {
+  return fused ? __fmaf_rn(a, b, c) : a * b + c;
+}
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
-                            float bc1, float bc2_sqrt) {
+                            float* __restrict__ v, int64_t n, float w1, float b2, float w2, float eps, float wd,
+                            float neg_step_size, float bc2_sqrt) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const float pi = p[i];
   float gi = g[i];
-  if (wd != 0.0f) gi = gi + wd * p[i];
-  float mi = m[i] + (gi - m[i]) * (1.0f - b1);  // torch lerp_
-  float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+  if (wd != 0.0f) gi = madd(YANERF_ADAM_FMA & 1, wd, pi, gi);         // torch._foreach_add(grads, params, alpha=wd)
+  const float mi = madd(YANERF_ADAM_FMA & 2, w1, gi - m[i], m[i]);     // lerp_(grad, 1 - beta1), weight < 0.5 branch
+  const float vi = madd(YANERF_ADAM_FMA & 4, w2 * gi, gi, v[i] * b2);  // mul_(beta2).addcmul_(g, g, 1 - beta2)
   m[i] = mi;
   v[i] = vi;
-  float denom = sqrtf(vi) / bc2_sqrt + eps;
-  p[i] = p[i] - (lr / bc1) * (mi / denom);
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;                     // (sqrt(v) / bc2_sqrt).add_(eps)
+  p[i] = madd(YANERF_ADAM_FMA & 8, neg_step_size, mi / denom, pi);     // addcdiv_(m, denom, value=-step_size)
 }
 
 }  // namespace yanerf
@@ -627,14 +641,18 @@ int yanerf_rgb_loss(const float* pred, const float* image, const float* xys, int
   return 0;
 }
 
-int yanerf_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
-                float beta1, float beta2, float eps, float weight_decay, int64_t step, void* stream) {
+int yanerf_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
+                double beta1, double beta2, double eps, double weight_decay, int64_t step, void* stream) {
   YN_CHECK(step >= 1, "adam: step must be >= 1");
+  YN_CHECK(params && grads && exp_avg && exp_avg_sq, "adam: null pointer");
   if (n == 0) return 0;
-  float bc1 = 1.0f - powf(beta1, (float)step);
-  float bc2 = 1.0f - powf(beta2, (float)step);
+  // the host-side scalars in double, as torch computes them in Python (adam.py: bias corrections, step size)
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  const double step_size = lr / bc1;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), params, grads,
-                     exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, bc1, sqrtf(bc2));
+                     exp_avg, exp_avg_sq, n, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
+                     (float)weight_decay, (float)(-step_size), (float)std::sqrt(bc2));
   YN_LAUNCH_CHECK("adam");
   return 0;
 }

@@ -44,22 +44,36 @@ def _f32c(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
 
 
 class _Rng:
-    """Philox (seed, offset) stream shared by all kernels; reseeded by torch.manual_seed."""
+    """Philox (seed, offset) stream. The module-level RNG (used by the registry ops) follows torch.manual_seed; a
+    stream built with an explicit seed (the fused trainer's, seed + rank as scripts/run.py:70-71 seeds each rank)
+    is independent of torch's global generator."""
 
-    def __init__(self):
-        self._seed = None
+    def __init__(self, seed: Optional[int] = None):
+        self._fixed = seed is not None
+        self._seed = None if seed is None else int(seed) & 0xFFFFFFFFFFFFFFFF
         self._offset = 0
 
     def next(self, n: int = 1) -> Tuple[int, int]:
-        seed = torch.initial_seed() & 0xFFFFFFFFFFFFFFFF
-        if seed != self._seed:
-            self._seed, self._offset = seed, 0
+        if not self._fixed:
+            seed = torch.initial_seed() & 0xFFFFFFFFFFFFFFFF
+            if seed != self._seed:
+                self._seed, self._offset = seed, 0
         off = self._offset
         self._offset += max(int(n), 1)
-        return seed, off
+        return self._seed, off
+
+    def get_state(self) -> Tuple[int, int]:
+        return self._seed, self._offset
+
+    def set_state(self, state: Tuple[int, int]) -> None:
+        self._seed, self._offset = state
 
 
 RNG = _Rng()
+
+
+def philox_stream(seed: int) -> _Rng:
+    return _Rng(seed)
 
 
 class _Injection:
@@ -80,7 +94,9 @@ INJECT = _Injection()
 
 @contextmanager
 def injected_randomness(**queues):
-    """with injected_randomness(pixel_ids=t, jitter_u=t, noise=[nc, nf], pdf_u=t): ..."""
+    """with injected_randomness(pixel_ids=t, jitter_u=t, noise=[nc, nf], pdf_u=t): ...
+    Consumed by the registry ops and by NeRFTrainer.step alike (pixel ids, stratified jitter, the coarse then the
+    fine density noise, the refinement uniforms), in the order the reference draws them."""
     INJECT.queues = {k: list(v) if isinstance(v, (list, tuple)) else [v] for k, v in queues.items()}
     try:
         yield

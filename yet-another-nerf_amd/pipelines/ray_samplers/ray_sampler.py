@@ -127,8 +127,9 @@ class RaySampler(torch.nn.Module):
                          lengths=z.view(B, *spatial, P), xys=xys.view(B, *spatial, 2))
 
     @staticmethod
-    def _weighted_ids(B, H, W, num_rays, mask, sampling_prob_mask, device):
-        """Pixel ids for masked / probability-weighted sampling (ray_sampler.py:181-227)."""
+    def _sampling_weights(B, H, W, num_rays, mask, sampling_prob_mask, device):
+        """The multinomial weights of masked / probability-weighted sampling (ray_sampler.py:181-216): [B, H*W], or
+        [B, L, H*W] for a layered (B, L, H, W) sampling_prob_mask (num_rays then a list of L counts)."""
         weights = mask.reshape(B, -1) if mask is not None else torch.ones(B, H * W, device=device)
         if sampling_prob_mask is not None:
             if tuple(sampling_prob_mask.shape) == (B, H, W):
@@ -147,6 +148,12 @@ class RaySampler(torch.nn.Module):
             else:
                 raise ValueError(f"Invalida `sampling_prob_mask`, shape of {sampling_prob_mask.shape}, want (B, H, W) "
                                  f"or (B, L, H, W)")
+        return weights, num_rays
+
+    @staticmethod
+    def _weighted_ids(B, H, W, num_rays, mask, sampling_prob_mask, device):
+        """Pixel ids for masked / probability-weighted sampling (ray_sampler.py:181-227)."""
+        weights, num_rays = RaySampler._sampling_weights(B, H, W, num_rays, mask, sampling_prob_mask, device)
         if weights.dim() == 2:
             return _safe_multinomial(weights, num_rays)
         return torch.cat([_safe_multinomial(weights[:, i], num_rays[i]) for i in range(len(num_rays))], dim=-1)

@@ -18,24 +18,10 @@ from typing import Dict, List, Optional, Sequence
 import torch
 
 from . import _C, ops, parallel
+from .lr_schedule import lr_at, scaled_lrs  # noqa: F401  (lr_at re-exported: train.lr_at)
 from .pipelines.models import MODELS
 
 F32 = torch.float32
-
-
-def lr_at(runner_cfg, it: int) -> float:
-    """Warm-up then exponential/cosine decay (runners/utils.py:65-109, applied per iteration in apis.py:66-68)."""
-    init = float(runner_cfg["init_lr"])
-    warm = int(runner_cfg.get("warmup_steps", 0))
-    if it < warm:
-        wl = float(runner_cfg.get("warmup_lr", init))
-        return min(init, wl + (init - wl) * it / max(warm, 1))
-    if runner_cfg.get("lr_decay_type", "exponential") == "exponential":
-        return max(float(runner_cfg["min_lr"]),
-                   init * float(runner_cfg["lr_decay_rate"]) ** (it / float(runner_cfg["lr_decay_iters"])))
-    mn = float(runner_cfg["min_lr"])
-    return (init - mn) * 0.5 * (1.0 + math.cos(math.pi * (it / float(runner_cfg["lr_decay_iters"])) /
-                                               float(runner_cfg["num_iters"]))) + mn
 
 
 class _Pass:
@@ -67,11 +53,20 @@ def _p(t):
 
 
 class NeRFTrainer:
-    def __init__(self, pipeline_cfg, *, precision: str = "fp32", device="cuda", lr: float = 5e-4,
-                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 42,
-                 n_rays: Optional[int] = None, overlap: Optional[bool] = None):
+    def __init__(self, pipeline_cfg, *, precision: str = "fp32", device="cuda", lr: Optional[float] = None,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: Optional[float] = None, seed: int = 42,
+                 n_rays: Optional[int] = None, overlap: Optional[bool] = None, runner_cfg=None):
+        """pipeline_cfg: the `pipeline:` section of a reference config (lego.yml / fern.yml).
+        runner_cfg: its `runner:` section. When given, every step uses the reference schedule
+        (lr_schedule.lr_at: decay, then warm-up; init_lr / min_lr linearly scaled by the world size under
+        torch.distributed, scripts/run.py:152-156) and its weight_decay; `lr` then must be None. Without it the
+        learning rate is the constant `lr` (default 5e-4).
+        seed: the weights are initialised from `seed` on every rank (then broadcast from rank 0, as DDP does); the
+        trainer's own Philox stream (pixel sampling, jitter, density noise, refinement) is keyed by seed + rank,
+        as scripts/run.py:70-71 seeds each rank. torch's global generator is left untouched."""
         self.dev = torch.device(device)
         rs, rd, mc = pipeline_cfg["ray_sampler"], pipeline_cfg["renderer"], pipeline_cfg["model"]
+        self._check_supported(pipeline_cfg)
         self.R = int(n_rays or rs["n_rays_per_image_sampled_from_mask"])
         self.Pc = int(rs["n_pts_per_ray_training"])
         self.Pn = int(rd["n_pts_per_ray_fine_training"])
@@ -90,17 +85,30 @@ class NeRFTrainer:
             background_density_bias=float(rd.get("background_density_bias", 0.0)),
             hard_background=bool(rd.get("hard_background", False)),
             bg_color=tuple(float(x) for x in rd.get("bg_color", (0.0,))))
-        torch.manual_seed(seed)
         mcfg = dict(mc)
         mcfg["precision"] = precision
-        self.models = [MODELS.build(dict(mcfg)).to(self.dev) for _ in range(2)]  # coarse, fine
+        with torch.random.fork_rng(devices=[]):  # seeded init without resetting the caller's generator
+            torch.manual_seed(seed)
+            self.models = [MODELS.build(dict(mcfg)).to(self.dev) for _ in range(2)]  # coarse, fine
         self.specs = [m.spec() for m in self.models]
         self.params: List[List[torch.nn.Parameter]] = [m.hip_params() for m in self.models]
         self.flat = parallel.FlatParams(self.params[0] + self.params[1])
         parallel.broadcast_(self.flat.data)
+        self.world, self.rank = parallel.world_rank()
+        self.rng = ops.philox_stream(int(seed) + self.rank)
         self.exp_avg = torch.zeros_like(self.flat.data)
         self.exp_avg_sq = torch.zeros_like(self.flat.data)
-        self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        self.runner_cfg = runner_cfg
+        if runner_cfg is not None:
+            if lr is not None:
+                raise ValueError("NeRFTrainer: pass either runner_cfg (the reference schedule) or a constant lr")
+            # the optimizer's init_lr (param_group["init_lr"], runners/utils.py:148-151), world-scaled
+            self.init_lr = scaled_lrs(runner_cfg, self.world)[0]
+            wd = runner_cfg.get("weight_decay", 0.0) if weight_decay is None else weight_decay
+        else:
+            self.init_lr = 5e-4 if lr is None else float(lr)
+            wd = 0.0 if weight_decay is None else weight_decay
+        self.lr, self.betas, self.eps, self.weight_decay = self.init_lr, betas, eps, float(wd)
         self.step_count = 0
         L = _C.lib()
         self.packed = [torch.empty(L.yanerf_mlp_packed_bytes(ctypes.byref(s.desc()), s.precision), dtype=torch.uint8,
@@ -126,6 +134,7 @@ class NeRFTrainer:
         self.grad_ptrs = [_C.ptr_array([p.grad.data_ptr() for p in ps]) for ps in self.params]
         self.param_ptrs = [_C.ptr_array([p.data_ptr() for p in ps]) for ps in self.params]
         self.events: Optional[Dict[str, List]] = None  # optional per-phase timing probes
+        self.kernel_probes = False  # serialise the backward kernels (per-kernel timing; see step())
         # evaluation (full-grid rendering) settings of the same configs (ray_sampler.py:54-56; renderer.py:29-52)
         self.Pc_eval = int(rs.get("n_pts_per_ray_evaluation", self.Pc))
         self.Pn_eval = int(rd.get("n_pts_per_ray_fine_evaluation", self.Pn))
@@ -155,55 +164,121 @@ class NeRFTrainer:
         return out
 
     # --------------------------------------------------------------------------------------- one step
-    def step(self, pose: torch.Tensor, focal: torch.Tensor, image: torch.Tensor, near: Optional[float] = None,
-             far: Optional[float] = None) -> Dict[str, torch.Tensor]:
-        """pose [1,3,4] (or [1,4,4]), focal [1], image [1,H,W,3] resident on the device; near/far override the
-        configured depth range (LLFF's per-image bounds, averaged as ray_sampler.py:280-283 does)."""
-        near = self.near if near is None else float(near)
-        far = self.far if far is None else float(far)
+    @staticmethod
+    def _check_supported(pipeline_cfg) -> None:
+        """Refuse (instead of silently ignoring) the reference options the fused step does not implement; the
+        registry NeRFPipeline runs them."""
+        rs, rd = pipeline_cfg["ray_sampler"], pipeline_cfg["renderer"]
+        lw = pipeline_cfg.get("loss_weights", None) or {}
+        for k, v in dict(lw).items():
+            if k not in ("loss_rgb_mse", "loss_prev_stage_rgb_mse") or float(v) != 1.0:
+                raise NotImplementedError(f"NeRFTrainer: loss_weights {dict(lw)} (the fused step computes "
+                                          f"loss_rgb_mse + loss_prev_stage_rgb_mse); use the registry NeRFPipeline")
+        if float(rs.get("scene_extent", 0.0) or 0.0) > 0.0:
+            raise NotImplementedError("NeRFTrainer: scene_extent > 0 (ray_sampler.py:100-110) is not supported")
+        if str(rs.get("sampling_mode_training", "mask_sample")) != "mask_sample":
+            raise NotImplementedError("NeRFTrainer: only MASK_SAMPLE training ray sampling is fused")
+        if int(pipeline_cfg.get("num_passes", 2)) != 2:
+            raise NotImplementedError("NeRFTrainer: the fused step renders exactly two passes (coarse, fine)")
+
+    def _check_inputs(self, pose, focal, image) -> None:
+        for name, t in (("pose", pose), ("focal", focal), ("image", image)):
+            if not isinstance(t, torch.Tensor) or t.device != self.dev or t.dtype != F32:
+                raise ValueError(f"NeRFTrainer.step: {name} must be a float32 tensor on {self.dev}")
+        C = self.specs[0].color_dim
+        if image.numel() != self.H * self.W * C or image.shape[-1] != C:
+            raise ValueError(f"NeRFTrainer.step: image of shape {tuple(image.shape)}, expected [1, {self.H}, "
+                             f"{self.W}, {C}] (the configured image size and color_dim)")
+        if pose.numel() not in (12, 16) or focal.numel() != 1:
+            raise ValueError(f"NeRFTrainer.step: one camera per step (pose {tuple(pose.shape)}, focal "
+                             f"{tuple(focal.shape)})")
+
+    def current_lr(self) -> float:
+        """The learning rate of the next step: the reference schedule at passed_iter = steps taken so far."""
+        if self.runner_cfg is None:
+            return self.lr
+        return lr_at(self.runner_cfg, self.step_count, self.world)
+
+    def step(self, pose: torch.Tensor, focal: torch.Tensor, image: torch.Tensor, near=None,
+             far=None) -> Dict[str, torch.Tensor]:
+        """One training step on one camera: pose [1,3,4] (or [1,4,4]), focal [1], image [1,H,W,C] float32, resident
+        on the device. near/far override the configured depth range: floats, or LLFF's per-image bound tensors,
+        which are averaged as _xy_to_ray_bundle does (ray_sampler.py:280-283).
+
+        Randomness comes from the trainer's Philox stream, or, inside ops.injected_randomness(...), from the
+        injected draws in the reference's order: pixel_ids [1,R] int64, jitter_u [1,R,Pc], noise (coarse [R,Pc],
+        then fine [R,Pf]), pdf_u [R,Pn]. The reference's training step is replayed that way by the parity tests."""
+        near = self.near if near is None else (near.float().mean().item() if isinstance(near, torch.Tensor)
+                                               else float(near))
+        far = self.far if far is None else (far.float().mean().item() if isinstance(far, torch.Tensor)
+                                            else float(far))
+        self._check_inputs(pose, focal, image)
         L = _C.lib()
         st = ops._stream()
         R = self.R
         pose = pose.reshape(1, -1, 4)[:, :3, :4].contiguous()
         focal = focal.reshape(1).contiguous()
-        image = image.reshape(1, self.H, self.W, -1)
+        image = image.reshape(1, self.H, self.W, -1).contiguous()
+        C = image.shape[-1]
+        inj_ids = ops.INJECT.take("pixel_ids")
+        inj_jit = ops.INJECT.take("jitter_u") if self.stratified else None
+        if inj_ids is not None:
+            inj_ids = inj_ids.to(self.dev, torch.int64).reshape(1, R).contiguous()
+        if inj_jit is not None:
+            inj_jit = inj_jit.to(self.dev, F32).reshape(1, R, self.Pc).contiguous()
         # pack the current parameters into the kernel layout (both models)
         for i, s in enumerate(self.specs):
             _C.check(L.yanerf_mlp_pack(ctypes.byref(s.desc()), s.precision, self.param_ptrs[i], _p(self.packed[i]),
                                        st), "yanerf_mlp_pack")
-        # rays: uniform pixel sampling without replacement + stratified depths (Philox)
-        seed, off = ops.RNG.next(R * self.Pc)
-        _C.check(L.yanerf_raygen(_p(pose), _p(focal), None, None, 1, R, self.W, self.H, float(self.W), float(self.H),
-                                 near, far, self.Pc, 2 if self.stratified else 0, None, seed, off, _p(self.o),
+        # rays: uniform pixel sampling without replacement + stratified depths (Philox, or injected draws)
+        seed, off = self.rng.next(R * self.Pc)
+        jmode = 0 if not self.stratified else (1 if inj_jit is not None else 2)
+        _C.check(L.yanerf_raygen(_p(pose), _p(focal), None, _p(inj_ids), 1, R, self.W, self.H, float(self.W),
+                                 float(self.H), near, far, self.Pc, jmode, _p(inj_jit), seed, off, _p(self.o),
                                  _p(self.d), _p(self.zc), _p(self.xys), None, st), "yanerf_raygen")
-        scale = 1.0 / (R * 3)
+        scale = 1.0 / (R * C)
         out = {}
         for k, (z, ps) in enumerate(((self.zc, self.passes[0]), (self.zf, self.passes[1]))):
             spec = self.specs[k]
             if k == 1:
-                seed, off = ops.RNG.next(R * self.Pn)
+                seed, off = self.rng.next(R * self.Pn)
+                u = ops.INJECT.take("pdf_u") if self.random_refine else None
+                if u is not None:
+                    u = u.to(self.dev, F32).reshape(R, self.Pn).contiguous()
                 _C.check(L.yanerf_refine(_p(self.zc), _p(self.passes[0].w), R, self.Pc, self.Pn,
-                                         0 if self.random_refine else 1, None, seed, off, int(self.append),
+                                         0 if self.random_refine else 1, _p(u), seed, off, int(self.append),
                                          _p(self.zf), st), "yanerf_refine")
             P = ps.P
             self._probe(f"mlp_fwd_{k}", lambda: _C.check(L.yanerf_mlp_forward(
                 ctypes.byref(ps.desc), spec.precision, _p(self.packed[k]), _p(self.o), _p(self.d), _p(z), R, P,
                 _p(ps.sigma), _p(ps.rgb), _p(ps.saved), st), "yanerf_mlp_forward"))
+            noise = None
             if self.noise_std > 0:
-                seed, off = ops.RNG.next(R * P)
-                o = self.march.opts(2, self.noise_std, seed, off)
+                noise = ops.INJECT.take("noise")
+                if noise is not None:
+                    noise = noise.to(self.dev, F32).reshape(R, P).contiguous()
+                    o = self.march.opts(1, self.noise_std)
+                else:
+                    seed, off = self.rng.next(R * P)
+                    o = self.march.opts(2, self.noise_std, seed, off)
             else:
                 o = self.march.opts(0, 0.0)
             _C.check(L.yanerf_composite_forward(ctypes.byref(o), _p(ps.sigma), _p(ps.rgb), _p(z), _p(self.d), None,
-                                                None, R, P, 3, _p(ps.feats), _p(ps.depth), _p(ps.alpha), _p(ps.w), st),
-                     "yanerf_composite_forward")
-            _C.check(L.yanerf_rgb_loss(_p(ps.feats), _p(image), _p(self.xys), 1, R, self.H, self.W, 3, scale,
+                                                _p(noise), R, P, C, _p(ps.feats), _p(ps.depth), _p(ps.alpha),
+                                                _p(ps.w), st), "yanerf_composite_forward")
+            _C.check(L.yanerf_rgb_loss(_p(ps.feats), _p(image), _p(self.xys), 1, R, self.H, self.W, C, scale,
                                        _p(ps.sq), _p(ps.g_feats), st), "yanerf_rgb_loss")
             _C.check(L.yanerf_composite_backward(ctypes.byref(o), _p(ps.sigma), _p(ps.rgb), _p(z), _p(self.d), None,
-                                                 None, _p(ps.g_feats), None, None, R, P, 3, _p(ps.g_sigma),
+                                                 _p(noise), _p(ps.g_feats), None, None, R, P, C, _p(ps.g_sigma),
                                                  _p(ps.g_rgb), st), "yanerf_composite_backward")
             out["sq_coarse" if k == 0 else "sq_fine"] = ps.sq
-        if self.side is None:
+        if self.kernel_probes:
+            # timing probe mode (bench.py's per-kernel roofline): every MLP backward kernel alone on the stream, in the
+            # order dX, dW, slab reduce; the result is identical to the other schedules
+            for k in (1, 0):
+                for ph in (1, 4, 8):
+                    self._mlp_backward(k, st, phase=ph)
+        elif self.side is None:
             self._mlp_backward(1, st)
             self._mlp_backward(0, st)
         elif self.overlap == "split":
@@ -223,6 +298,7 @@ class NeRFTrainer:
             self._mlp_backward(1, st)
             torch.cuda.current_stream().wait_stream(self.side)
         parallel.allreduce_mean_(self.flat.grad)
+        self.lr = self.current_lr()  # the reference schedules before the step (apis.py:66-68)
         self.step_count += 1
         _C.check(L.yanerf_adam(_p(self.flat.data), _p(self.flat.grad), _p(self.exp_avg), _p(self.exp_avg_sq),
                                self.flat.numel, float(self.lr), float(self.betas[0]), float(self.betas[1]),
@@ -232,7 +308,7 @@ class NeRFTrainer:
     def _mlp_backward(self, k: int, st, stream=None, phase: int = 3):
         L = _C.lib()
         ps, spec = self.passes[k], self.specs[k]
-        name = f"mlp_bwd_{k}" if phase == 3 else f"mlp_bwd{phase}_{k}"
+        name = {3: "mlp_bwd", 1: "mlp_dx", 2: "mlp_dwr", 4: "mlp_dw", 8: "mlp_reduce"}[phase] + f"_{k}"
         self._probe(name, lambda: _C.check(L.yanerf_mlp_backward_phase(
             ctypes.byref(ps.desc), spec.precision, _p(self.packed[k]), _p(ps.saved), _p(ps.rgb), _p(ps.g_sigma),
             _p(ps.g_rgb), self.R, ps.P, self.grad_ptrs[k], _p(self.ws[k]), phase, st), "yanerf_mlp_backward"), stream)
@@ -287,7 +363,7 @@ class NeRFTrainer:
         for r0 in range(0, n, R):
             r = min(R, n - r0)
             ids = torch.arange(p0 + r0, p0 + r0 + r, device=self.dev, dtype=torch.int64)
-            seed, off = ops.RNG.next(r * self.Pc_eval)
+            seed, off = self.rng.next(r * self.Pc_eval)
             _C.check(L.yanerf_raygen(_p(pose), _p(focal), None, _p(ids), 1, r, W, H, float(self.W), float(self.H),
                                      near, far, self.Pc_eval, 2 if self.stratified_eval else 0, None, seed, off,
                                      _p(b["o"]), _p(b["d"]), _p(b["zc"]), _p(b["xys"]), None, st), "yanerf_raygen")
@@ -296,7 +372,7 @@ class NeRFTrainer:
                 spec = self.specs[k]
                 P = self.Pc_eval if k == 0 else zs[1].shape[1]
                 if k == 1:
-                    seed, off = ops.RNG.next(r * self.Pn_eval)
+                    seed, off = self.rng.next(r * self.Pn_eval)
                     _C.check(L.yanerf_refine(_p(b["zc"]), _p(b["w"]), r, self.Pc_eval, self.Pn_eval,
                                              0 if self.random_refine_eval else 1, None, seed, off, int(self.append),
                                              _p(b["zf"]), st), "yanerf_refine")
@@ -354,7 +430,8 @@ class NeRFTrainer:
     def optimizer_state_dict(self) -> Dict:
         from . import checkpoint
         return checkpoint.adam_state_from_flat(self.params[0] + self.params[1], self.exp_avg, self.exp_avg_sq,
-                                               self.step_count, self.lr, self.betas, self.eps, self.weight_decay)
+                                               self.step_count, self.lr, self.betas, self.eps, self.weight_decay,
+                                               init_lr=self.init_lr)
 
     def load_optimizer_state_dict(self, osd: Dict):
         from . import checkpoint
@@ -362,6 +439,7 @@ class NeRFTrainer:
         self.step_count = step or 0
         g = osd.get("param_groups", [{}])[0]
         self.lr = float(g.get("lr", self.lr))
+        self.init_lr = float(g.get("init_lr", self.init_lr))
         self.betas = tuple(g.get("betas", self.betas))
         self.eps = float(g.get("eps", self.eps))
         self.weight_decay = float(g.get("weight_decay", self.weight_decay))

@@ -15,7 +15,7 @@ import pytest
 import torch
 
 from oracle import nerf_oracle as O
-from parity_gates import split_gate
+from parity_gates import oracle_fine_at, split_gate
 from weights import LEGO_ARCH, make_nerf_mlp_params
 
 pytestmark = pytest.mark.gpu
@@ -60,6 +60,7 @@ def test_fern_render_with_tensor_bounds_vs_oracle(n_fine):
     pipe.eval()
     pose = forward_pose()
     H, W = 9, 12
+    # depths here reach FAR = 7.25 (Lego: 6): the depth gate is 1.5e-4 (2e-5 of the far bound, Lego's relative gate)
     near_t, far_t = torch.tensor([[NEAR]], device=DEV), torch.tensor([[FAR]], device=DEV)
     with torch.no_grad():
         rb = pipe.ray_sampler(t(pose[None]), t([FOCAL]), evaluation_mode=EvaluationMode.EVALUATION, image_height=H,
@@ -76,8 +77,10 @@ def test_fern_render_with_tensor_bounds_vs_oracle(n_fine):
     np.testing.assert_allclose(n(ro.prev_stage.depths).reshape(R), ref["coarse"][1].reshape(R), atol=1e-4, rtol=0)
     from yanerf_amd import ops
     z_gpu = n(ops.refine(rb.lengths.reshape(R, 64), ro.prev_stage.aux["weights"].reshape(R, 64), n_fine, det=True))
+    fine_at = oracle_fine_at(O, params[1], O.MLPArch.from_dict(LEGO_ARCH), o, d,
+                             O.RaymarchOpts(background_density_bias=1e-6))
     split_gate(n(ro.features).reshape(R, 3), ref["fine"][0], z_gpu, ref["z_fine"], n(ro.depths).reshape(R),
-               ref["fine"][1].reshape(R), tag=f"fern 64+{n_fine}")
+               ref["fine"][1].reshape(R), fine_at=fine_at, strict_depth=1.5e-4, tag=f"fern 64+{n_fine}")
     assert np.abs(ref["fine"][0]).max() > 1e-3
 
 

@@ -12,7 +12,7 @@ import pytest
 import torch
 
 from oracle import nerf_oracle as O
-from parity_gates import split_gate
+from parity_gates import oracle_fine_at, split_gate
 from weights import LEGO_ARCH, SMALL_ARCH, make_nerf_mlp_params
 
 pytestmark = pytest.mark.gpu
@@ -368,8 +368,11 @@ def test_render_eval_lego(pkg, golden, precision):
     # end-to-end: strict on every ray whose refined depths (from our coarse weights) equal the ones from the
     # reference's coarse weights; the others are counted boundary flips (parity_gates.split_gate)
     z_gpu = n(ops.refine(rb.lengths.reshape(R, -1), pv.aux["weights"].reshape(R, -1), 128, det=True))
+    o_r, d_r, _, _ = O.sample_rays_eval(g["pose"], g["focal"], 800, 800, 2.0, 6.0, 64, H=H, W=W)
+    fine_at = oracle_fine_at(O, make_nerf_mlp_params(LEGO_ARCH, int(g["seeds"][1])), O.MLPArch.from_dict(LEGO_ARCH),
+                             o_r, d_r, O.RaymarchOpts(background_density_bias=1e-6))
     split_gate(n(preds["rendered_images"]), g["rendered_images"], z_gpu, n(zf), n(preds["rendered_depths"]),
-               g["rendered_depths"], tag=f"render_eval_lego {precision}")
+               g["rendered_depths"], fine_at=fine_at, tag=f"render_eval_lego {precision}")
     close(n(preds["loss_rgb_mse"]), g["loss_rgb_mse"], 2e-6)
 
 
@@ -455,8 +458,10 @@ def test_fern_config_render_vs_oracle(pkg):
     close(n(ro.prev_stage.features).reshape(R, 3), ref["coarse"][0], 1e-5)
     close(n(ro.prev_stage.depths).reshape(R), ref["coarse"][1].reshape(R), 1e-4)
     z_gpu = n(pkg["ops"].refine(rb.lengths.reshape(R, 64), ro.prev_stage.aux["weights"].reshape(R, 64), 64, det=True))
+    fine_at = oracle_fine_at(O, params[1], O.MLPArch.from_dict(LEGO_ARCH), o, d,
+                             O.RaymarchOpts(background_density_bias=1e-6))
     split_gate(n(ro.features).reshape(R, 3), ref["fine"][0], z_gpu, ref["z_fine"], n(ro.depths).reshape(R),
-               ref["fine"][1].reshape(R), tag="fern 64+64")
+               ref["fine"][1].reshape(R), fine_at=fine_at, tag="fern 64+64")
 
 
 def test_chunking_invariance(pkg, golden):
@@ -504,9 +509,8 @@ def test_trainer_checkpoint_interop(pkg, tmp_path):
     checkpoint.load_checkpoint(path, tr2)
     assert tr2.step_count == 2
     assert torch.equal(tr2.flat.data, tr.flat.data) and torch.equal(tr2.exp_avg_sq, tr.exp_avg_sq)
-    rng = (ops.RNG._seed, ops.RNG._offset)
+    tr2.rng.set_state(tr.rng.get_state())  # the same Philox position for the next draws
     tr.step(poses[2], focal, image)
-    ops.RNG._seed, ops.RNG._offset = rng
     tr2.step(poses[2], focal, image)
     torch.cuda.synchronize()
     assert torch.equal(tr2.flat.data, tr.flat.data)

@@ -15,10 +15,11 @@ def fma32(a, b, c):
     return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(np.float32)
 
 
-FLAGS = ("lerp_fma", "addcmul_fma", "wd_fma", "div_by_reciprocal", "addcdiv_fma", "addcdiv_scale_first")
+FLAGS = ("lerp_fma", "addcmul_fma", "wd_fma", "div_by_reciprocal", "addcdiv_fma", "addcdiv_scale_first",
+         "addcmul_gg_first")
 
 
-def emulate(p, g, m, v, step, lr, b1, b2, eps, wd, f_lerp, f_cmul, f_wd, f_recip, f_cdiv, f_sf):
+def emulate(p, g, m, v, step, lr, b1, b2, eps, wd, f_lerp, f_cmul, f_wd, f_recip, f_cdiv, f_sf, f_gg):
     f32 = np.float32
     if wd != 0:
         g = fma32(np.full_like(p, f32(wd)), p, g) if f_wd else (g + (f32(wd) * p).astype(np.float32)).astype(f32)
@@ -26,8 +27,13 @@ def emulate(p, g, m, v, step, lr, b1, b2, eps, wd, f_lerp, f_cmul, f_wd, f_recip
     d = (g - m).astype(np.float32)
     m2 = fma32(np.full_like(d, w1), d, m) if f_lerp else (m + (w1 * d).astype(np.float32)).astype(np.float32)
     v1 = (v * f32(b2)).astype(np.float32)
-    a2 = (f32(1 - b2) * g).astype(np.float32)
-    v2 = fma32(a2, g, v1) if f_cmul else (v1 + (a2 * g).astype(np.float32)).astype(np.float32)
+    if f_gg:  # foreach addcmul: self + value * (t1 * t2)
+        gg = (g * g).astype(np.float32)
+        v2 = fma32(np.full_like(gg, f32(1 - b2)), gg, v1) if f_cmul else \
+            (v1 + (f32(1 - b2) * gg).astype(np.float32)).astype(np.float32)
+    else:
+        a2 = (f32(1 - b2) * g).astype(np.float32)
+        v2 = fma32(a2, g, v1) if f_cmul else (v1 + (a2 * g).astype(np.float32)).astype(np.float32)
     bc1 = 1 - b1 ** step
     bc2 = 1 - b2 ** step
     ss = f32(-(lr / bc1))
@@ -75,12 +81,14 @@ def main():
                 pn, mn, vn = tp, tm, tv  # continue from torch's state
             out[f"foreach={foreach}"] = matches
         res[f"wd={wd}"] = out
-    full = {}
+    full, best = {}, {}
     for wd, o in res.items():
         for k, m in o.items():
             full[f"{wd} {k}"] = [dict(zip(FLAGS, eval(fl))) for fl, v in m.items()
                                  if all(x == n for step in v for x in step)]
-    print(json.dumps({"device": dev, "n": n, "bit_exact_emulations": full}))
+            ranked = sorted(m.items(), key=lambda kv: -sum(x for step in kv[1] for x in step))[:4]
+            best[f"{wd} {k}"] = [(dict(zip(FLAGS, eval(fl))), v) for fl, v in ranked]
+    print(json.dumps({"device": dev, "n": n, "bit_exact_emulations": full, "best": best}))
 
 
 if __name__ == "__main__":

@@ -996,10 +996,15 @@ __device__ __forceinline__ void copy_tile_pm(const typename Cfg<T>::lds_t* act, 
     f4 v[GRP];
 #pragma unroll
     for (int i = 0; i < GRP; ++i) v[i] = lds_chunk<T>(act, m0 + (NTHR / CPR) * (i0 + i), col0 / 8 + c);
+    // The chunk offset goes into the VGPR offset with soffset = 0, NOT into soffset: gfx950 has a write-after-read
+    // hazard between a 128-bit buffer store's data VGPRs and a following VALU write of them, which LLVM's hazard
+    // recognizer only covers when soffset is not a register (GCNHazardRecognizer::createsVALUHazard). With an SGPR
+    // soffset the compiler reused a data VGPR in the next instruction and, under load (another kernel on the
+    // chip), the store took the new value for some lanes: tools/debug_bf16_overlap.py, dZc rows 32..47 of a tile.
 #pragma unroll
     for (int i = 0; i < GRP; ++i)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint32_t __attribute__((ext_vector_type(4))), v[i]), rs,
-                                             goff, (i0 + i) * NTHR * 16, 0);
+                                             goff + (uint32_t)((i0 + i) * NTHR * 16), 0, 0);
   }
 }
 

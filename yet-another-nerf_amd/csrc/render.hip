@@ -515,15 +515,10 @@ __global__ void rgb_loss_kernel(const float* __restrict__ pred, const float* __r
 
 // torch.optim.Adam's per-element arithmetic (torch/optim/adam.py _multi_tensor_adam, the default on the GPU), op for
 // op: the scalars arrive already rounded to float from the host's double arithmetic, exactly as torch casts its
-// Python-float scalars; which of the multiply-adds torch's own kernels fuse is YANERF_ADAM_FMA (bit 0 weight decay
-// `grad + wd * p`, bit 1 lerp `m + w1 * (g - m)`, bit 2 addcmul `v*b2 + (w2 * g) * g`, bit 3 addcdiv
-// `p + (-step_size) * (m / denom)`), pinned by tools/adam_emulation_check.py on the GPU.
-#ifndef YANERF_ADAM_FMA
-#define YANERF_ADAM_FMA 15
-#endif
-__device__ __forceinline__ float madd(bool fused, float a, float b, float c) {
-  return fused ? __fmaf_rn(a, b, c) : a * b + c;
-}
+// Python-float scalars, and the multiply-adds are fused where torch's foreach kernels fuse them. Pinned bit for bit by
+// tools/adam_emulation_check.py against torch on the MI355X (foreach: weight decay `grad + wd * p`, lerp
+// `m + w1 * (g - m)`, addcmul `v * b2 + w2 * (g * g)` and addcdiv `p + (-step_size) * (m / denom)` all fused; the
+// denominator a true division) and by tests/test_gpu_trainer.py::test_adam_matches_torch_adam.
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, int64_t n, float w1, float b2, float w2, float eps, float wd,
                             float neg_step_size, float bc2_sqrt) {
@@ -531,13 +526,13 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   if (i >= n) return;
   const float pi = p[i];
   float gi = g[i];
-  if (wd != 0.0f) gi = madd(YANERF_ADAM_FMA & 1, wd, pi, gi);         // torch._foreach_add(grads, params, alpha=wd)
-  const float mi = madd(YANERF_ADAM_FMA & 2, w1, gi - m[i], m[i]);     // lerp_(grad, 1 - beta1), weight < 0.5 branch
-  const float vi = madd(YANERF_ADAM_FMA & 4, w2 * gi, gi, v[i] * b2);  // mul_(beta2).addcmul_(g, g, 1 - beta2)
+  if (wd != 0.0f) gi = __fmaf_rn(wd, pi, gi);             // torch._foreach_add(grads, params, alpha=weight_decay)
+  const float mi = __fmaf_rn(w1, gi - m[i], m[i]);       // _foreach_lerp_(exp_avgs, grads, 1 - beta1)
+  const float vi = __fmaf_rn(w2, gi * gi, v[i] * b2);    // _foreach_mul_(beta2); _foreach_addcmul_(g, g, 1 - beta2)
   m[i] = mi;
   v[i] = vi;
-  const float denom = sqrtf(vi) / bc2_sqrt + eps;                     // (sqrt(v) / bc2_sqrt).add_(eps)
-  p[i] = madd(YANERF_ADAM_FMA & 8, neg_step_size, mi / denom, pi);     // addcdiv_(m, denom, value=-step_size)
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;        // _foreach_sqrt; _foreach_div_(bc2_sqrt); _foreach_add_(eps)
+  p[i] = __fmaf_rn(neg_step_size, mi / denom, pi);        // _foreach_addcdiv_(params, exp_avgs, denom, -step_size)
 }
 
 }  // namespace yanerf

@@ -25,7 +25,8 @@ def main(steps=20, rounds=3):
     focal = torch.tensor([0.5 * 800 / math.tan(0.5 * 0.6911112)], device=dev)
     res = {}
     for prec in (sys.argv[1].split(",") if len(sys.argv) > 1 else ("fp32", "bf16", "fp32x3")):
-        trs = {ov: NeRFTrainer(cfg.pipeline, precision=prec, device=dev, overlap=ov) for ov in (False, "both", "split")}
+        modes = (False, "both", "split", "early")
+        trs = {ov: NeRFTrainer(cfg.pipeline, precision=prec, device=dev, overlap=ov) for ov in modes}
         best = {ov: float("inf") for ov in trs}
         for r in range(rounds):
             for ov, tr in trs.items():
@@ -38,7 +39,7 @@ def main(steps=20, rounds=3):
                 torch.cuda.synchronize()
                 best[ov] = min(best[ov], (time.perf_counter() - t0) / steps * 1e3)
         res[prec] = {"ms_serial": round(best[False], 3), "ms_overlap": round(best["both"], 3),
-                     "ms_split": round(best["split"], 3)}
+                     "ms_split": round(best["split"], 3), "ms_early": round(best["early"], 3)}
         del trs
     print(json.dumps(res))
 

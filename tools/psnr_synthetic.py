@@ -29,7 +29,7 @@ from yanerf_amd.train import NeRFTrainer  # noqa: E402
 from yanerf_amd.utils.config import Config  # noqa: E402
 
 
-def run(data_dir: Path, precision: str, steps: int, dev, n_rays=4096, log=None):
+def run(data_dir: Path, precision: str, steps: int, dev, n_rays=4096, log=None, save=None):
     train = DeviceImageSet(BlenderDataset(str(data_dir), "train"), dev)
     test = DeviceImageSet(BlenderDataset(str(data_dir), "test", test_skip=1), dev)
     cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml"))
@@ -54,6 +54,9 @@ def run(data_dir: Path, precision: str, steps: int, dev, n_rays=4096, log=None):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     ev = tr.evaluate(test)
+    if save:  # reference-format checkpoint of the trained models (analysis of trained activations / gradients)
+        from yanerf_amd import checkpoint
+        checkpoint.save_checkpoint(str(save), tr, epoch=steps)
     res = {"precision": precision, "steps": steps, "rays_per_step": n_rays, "train_s": round(dt, 2),
            "rays_per_s": round(steps * n_rays / dt, 1), "test_psnr_fine": round(ev["loss_rgb_psnr"], 3),
            "test_psnr_coarse": round(ev["loss_prev_stage_rgb_psnr"], 3), "test_views": len(test)}
@@ -68,12 +71,13 @@ def main():
     ap.add_argument("--size", type=int, default=100)
     ap.add_argument("--precisions", default="fp32,fp32x3,bf16")
     ap.add_argument("--data", default=None, help="existing scene dir (default: generate into a temp dir)")
+    ap.add_argument("--save", default=None, help="write the last run's trained checkpoint to this file")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     with tempfile.TemporaryDirectory() as tmp:
         data = Path(a.data) if a.data else write_scene(Path(tmp) / "synthetic", a.size, 40, 8, device="cuda")
         out = {"scene": f"procedural blobs, {a.size}x{a.size}, 40 train / 8 test views, Lego config 64+128",
-               "runs": [run(data, p, a.steps, dev, log=sys.stderr) for p in a.precisions.split(",")]}
+               "runs": [run(data, p, a.steps, dev, log=sys.stderr, save=a.save) for p in a.precisions.split(",")]}
     print(json.dumps(out))
 
 

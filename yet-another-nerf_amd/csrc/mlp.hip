@@ -27,7 +27,8 @@
 
 // Development-only timing ablations (never set in the product build): 1 = no MFMA, 2 = no harmonic embedding,
 // 4 = no saved stores in the trunk epilogue, 8 = no VALU heads, 16 = no trunk LDS writes, 32 = no trunk barriers,
-// 64 = dX colour-head backward without its mask / weight math, 128 = dX without its point-major copies.
+// 64 = dX colour-head backward without its mask / weight math, 128 = dX without its point-major copies, 256 = bf16
+// GEMMs read only the first K-block of weights (L1-resident: the weight stream from L2 removed).
 #ifndef YANERF_F32_DB
 #define YANERF_F32_DB 0  // fp32 GEMM loop: double-buffered weight fragments (0: one set + copy, the earlier loop)
 #endif
@@ -198,8 +199,50 @@ __host__ __device__ inline int64_t row_ld(int64_t Npad, size_t es) {
   if ((units & 1) == 0) ++units;
   return units * 256 / (int64_t)es;
 }
+// bf16 point-major saves (Cfg<bf16_t>::PM): the non-negative (post-ReLU) sections -- H_0..H_{L-1} and the colour hidden
+// C, 2,176 of the 2,528 values a point saves -- are stored as fp8 e4m3 (OCP e4m3fn, 1 byte; values clamped to its 448
+// maximum, round to nearest even by v_cvt_scalef32_pk_fp8_bf16; exact-RNE against the e4m3fn definition on the MI355X:
+// tools/probes/probe_fp8.hip), the signed ones (PE, Y, dir-PE) stay bf16. They are the weight gradients' X operands
+// only (the dX kernel uses the ReLU mask words, never the activations), and the dW tile widens them back to bf16 (exact)
+// for the bf16 MFMA. Measured on a trained model (procedural scene, 3k steps): dW relative L2 error 0.6-0.9 % from the
+// fp8 rounding, against 0.03 % from bf16 storage and >10 % from the bf16 forward chain itself. Layout: byte offsets of
+// [Npad][width] sections. YANERF_BF16_A8=0 keeps every section in bf16 (A/B builds).
+#ifndef YANERF_BF16_A8
+#define YANERF_BF16_A8 1
+#endif
+constexpr int PM_HB = YANERF_BF16_A8 ? 1 : 2;  // bytes per saved H / C element
+struct PmSave {
+  int64_t pe, h0, y, dpe, c, total;
+};
+__host__ __device__ inline PmSave pm_save(int L, int64_t Npad) {
+  PmSave s;
+  int64_t o = 0;
+  s.pe = o; o += 2LL * KPE * Npad;
+  s.h0 = o; o += (int64_t)PM_HB * 256 * L * Npad;
+  s.y = o; o += 2LL * 256 * Npad;
+  s.dpe = o; o += 2LL * KDIR * Npad;
+  s.c = o; o += (int64_t)PM_HB * HC * Npad;
+  s.total = o;
+  return s;
+}
+// byte offset and element bytes of the saved section that starts at SavedRows row r0 (point-major bf16 layout)
+static int64_t pm_sec_bytes(int L, int64_t Npad, int64_t r0, int* es) {
+  const SavedRows SR = saved_rows(L);
+  const PmSave PS = pm_save(L, Npad);
+  *es = 2;
+  if (r0 == SR.pe) return PS.pe;
+  if (r0 >= SR.h0 && r0 < SR.y) {
+    *es = PM_HB;
+    return PS.h0 + (r0 - SR.h0) / 256 * (int64_t)PM_HB * 256 * Npad;
+  }
+  if (r0 == SR.y) return PS.y;
+  if (r0 == SR.dpe) return PS.dpe;
+  *es = PM_HB;
+  return PS.c;  // r0 == SR.c
+}
 static int64_t saved_t_bytes(int L, int64_t Npad, size_t es, bool pm) {
-  return saved_rows(L).rows * (pm ? Npad : row_ld(Npad, es)) * (int64_t)es;
+  if (pm) return pm_save(L, Npad).total;
+  return saved_rows(L).rows * row_ld(Npad, es) * (int64_t)es;
 }
 
 static int64_t tile_m(int prec) {
@@ -484,7 +527,7 @@ __device__ __forceinline__ void ring_fill(ARing<T, NT>& R, const typename Cfg<T>
     constexpr int D = Cfg<T>::APREF, EPC = Cfg<T>::EPC, KB = Cfg<T>::KB, FRAG = 64 * EPC, NP = Cfg<T>::PLANES;
 #pragma unroll
     for (int r = 0; r < D; ++r) {
-      const int k = r < nkb ? r : nkb - 1;
+      const int k = (YANERF_ABLATE & 256) ? 0 : (r < nkb ? r : nkb - 1);
 #pragma unroll
       for (int pl = 0; pl < NP; ++pl)
 #pragma unroll
@@ -628,7 +671,7 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
         for (int mt = 0; mt < MH; ++mt) acc[nt][mt + MH] = mma_blk<T>(ar[nt], b1[mt], acc[nt][mt + MH]);
       __builtin_amdgcn_sched_barrier(0);
       if (refill) {
-        const int ka = kb + D < nkb ? kb + D : nkb - 1;
+        const int ka = (YANERF_ABLATE & 256) ? 0 : (kb + D < nkb ? kb + D : nkb - 1);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) ar[nt] = *(const f4*)(wp[nt] + ka * FRAG);
       }
@@ -1008,6 +1051,60 @@ __device__ __forceinline__ void copy_tile_pm(const typename Cfg<T>::lds_t* act, 
   }
 }
 
+// The fp8 save of a point-major section (YANERF_BF16_A8): like copy_tile_pm, but a lane reads two 16-byte LDS chunks
+// (16 bf16 features of one point), converts them to 16 fp8 e4m3 (clamped to 448: the tile holds post-ReLU values, so
+// an integer min on the bf16 bits is the clamp) and writes one 16-byte chunk; a wave-instruction writes 1 KiB
+// contiguously.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t fp8x4_from_bf16(uint32_t w0, uint32_t w1) {
+  const u16x2 cap = {0x43E0, 0x43E0};  // 448.0 in bf16
+  const u16x2 a = __builtin_elementwise_min(__builtin_bit_cast(u16x2, w0), cap);
+  const u16x2 b = __builtin_elementwise_min(__builtin_bit_cast(u16x2, w1), cap);
+  i16x2 r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(i16x2{0, 0}, __builtin_bit_cast(bf16x2, a), 1.0f, false);
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, __builtin_bit_cast(bf16x2, b), 1.0f, true);
+  return __builtin_bit_cast(uint32_t, r);
+}
+template <typename T, int NTHR, int W>
+__device__ __forceinline__ void copy_tile_pm_fp8(const typename Cfg<T>::lds_t* act, int col0, uint8_t* dst, int tid) {
+  static_assert(sizeof(typename Cfg<T>::lds_t) == 2 && !is_x3<T>, "fp8 save: bf16 tiles");
+  constexpr int M = Cfg<T>::M, OPR = W / 16, TOT = M * OPR, IT = TOT / NTHR;
+  static_assert(TOT % NTHR == 0 && NTHR % OPR == 0, "copy_tile_pm_fp8: whole chunks / rows per pass");
+  constexpr int GRP = IT < 4 ? IT : 4;
+  int t = tid;
+  asm volatile("" : "+v"(t));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
+  const int m0 = t / OPR, j = t % OPR;
+  const uint32_t goff = (uint32_t)(t * 16);
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int i0 = 0; i0 < IT; i0 += GRP) {
+    f4 lo[GRP], hi[GRP];
+#pragma unroll
+    for (int i = 0; i < GRP; ++i) {
+      const int m = m0 + (NTHR / OPR) * (i0 + i);
+      lo[i] = lds_chunk<T>(act, m, col0 / 8 + 2 * j);
+      hi[i] = lds_chunk<T>(act, m, col0 / 8 + 2 * j + 1);
+    }
+#pragma unroll
+    for (int i = 0; i < GRP; ++i) {
+      const u32x4 out = {fp8x4_from_bf16(__float_as_uint(lo[i].x), __float_as_uint(lo[i].y)),
+                         fp8x4_from_bf16(__float_as_uint(lo[i].z), __float_as_uint(lo[i].w)),
+                         fp8x4_from_bf16(__float_as_uint(hi[i].x), __float_as_uint(hi[i].y)),
+                         fp8x4_from_bf16(__float_as_uint(hi[i].z), __float_as_uint(hi[i].w))};
+      // offset in the VGPR offset, soffset = 0 (the wide-store hazard note at copy_tile_pm)
+      __builtin_amdgcn_raw_buffer_store_b128(out, rs, goff + (uint32_t)((i0 + i) * NTHR * 16), 0, 0);
+    }
+  }
+}
+// save of a post-ReLU section: fp8 (YANERF_BF16_A8) or bf16
+template <typename T, int NTHR, int W>
+__device__ __forceinline__ void save_relu_pm(const typename Cfg<T>::lds_t* act, int col0, char* dst, int tid) {
+  if constexpr (YANERF_BF16_A8) copy_tile_pm_fp8<T, NTHR, W>(act, col0, (uint8_t*)dst, tid);
+  else copy_tile_pm<T, NTHR, W>(act, col0, (typename Cfg<T>::st_t*)dst, tid);
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global stores (the
 // saved rows / gradients / masks written between barriers are read by later kernels only). __syncthreads() is a
 // workgroup fence as well and waits for every outstanding store (vmcnt(0)) at each of the ~24 barriers per tile.
@@ -1043,6 +1140,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   const bool sv = STAT ? SAVE : saved != nullptr;
   const int64_t wpl = lay.t_plane;
   const SavedRows SR = saved_rows(lay.L);
+  const PmSave PS = pm_save(lay.L, Npad);  // byte offsets of the point-major sections (bf16)
   const int mt_ = tid / TPP, q = tid % TPP;
   const int64_t p = p0 + mt_;
   const int64_t pc = p < N ? p : N - 1;
@@ -1086,9 +1184,9 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     if constexpr (PM) {
       if (sv && !(YANERF_ABLATE & 4)) {
         if (l == 0) {
-          copy_tile_pm<T, NTHR, KPE>(act, PE_COL, saved + SR.pe * Npad + p0 * KPE, tid);
+          copy_tile_pm<T, NTHR, KPE>(act, PE_COL, (ST*)((char*)saved + PS.pe) + p0 * KPE, tid);
         } else {
-          copy_tile_pm<T, NTHR, 256>(act, 0, saved + (SR.h0 + 256LL * (l - 1)) * Npad + p0 * 256, tid);
+          save_relu_pm<T, NTHR, 256>(act, 0, (char*)saved + PS.h0 + ((l - 1) * Npad + p0) * 256LL * PM_HB, tid);
 #pragma unroll
           for (int w = 0; w < MW; ++w)
             masks[((((int64_t)(l - 1) * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
@@ -1146,7 +1244,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   ring_fill<T, NTC>(ringc, Wt + lay.wc_off, wpl, KC, crow0, KC / KB, lane);
   if constexpr (PM) {
     if (sv && !(YANERF_ABLATE & 4)) {
-      copy_tile_pm<T, NTHR, 256>(act, 0, saved + (SR.h0 + 256LL * (lay.L - 1)) * Npad + p0 * 256, tid);
+      save_relu_pm<T, NTHR, 256>(act, 0, (char*)saved + PS.h0 + ((lay.L - 1) * Npad + p0) * 256LL * PM_HB, tid);
 #pragma unroll
       for (int w = 0; w < MW; ++w)
         masks[((((int64_t)(lay.L - 1) * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
@@ -1183,8 +1281,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     gemm_lds<T, NTC, MT>(Wt + lay.wc_off, wpl, KC, crow0, act, 0, KC / KB, accc, lane, Wf + lay.bc_off, &ringc);
     if constexpr (PM) {
       if (sv) {
-        copy_tile_pm<T, NTHR, 256>(act, 0, saved + SR.y * Npad + p0 * 256, tid);
-        copy_tile_pm<T, NTHR, KDIR>(act, PE_COL, saved + SR.dpe * Npad + p0 * KDIR, tid);
+        copy_tile_pm<T, NTHR, 256>(act, 0, (ST*)((char*)saved + PS.y) + p0 * 256, tid);
+        copy_tile_pm<T, NTHR, KDIR>(act, PE_COL, (ST*)((char*)saved + PS.dpe) + p0 * KDIR, tid);
       }
     }
     lds_barrier();
@@ -1230,7 +1328,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     }
   }
   if constexpr (PM) {
-    if (sv) copy_tile_pm<T, NTHR, HC>(act, 0, saved + SR.c * Npad + p0 * HC, tid);  // C is still in the tile
+    if (sv) save_relu_pm<T, NTHR, HC>(act, 0, (char*)saved + PS.c + p0 * (int64_t)HC * PM_HB, tid);  // C still in LDS
   }
 }
 
@@ -1442,6 +1540,7 @@ struct DwJob {
   // a_chunks = 16-byte chunks of A per point that hold data; the tile's column space is "virtual": X0's columns
   // padded to x0p (a multiple of 8), then X1's (ktot_v = x0p + x1_rows); k-tiles are laid over ktot_v
   int a_ld, a_chunks, x0_ld, x1_ld, x0p, ktot_v;
+  int x0_u8, x1_u8;  // X0 / X1 stored as fp8 e4m3 (YANERF_BF16_A8: the post-ReLU sections); a k-tile is one format
 };
 constexpr int kMaxDwJobs = MAXL + 4;
 struct DwJobs {
@@ -1742,13 +1841,40 @@ __device__ __forceinline__ f4 pm_frag(const char* img, int f0, int lane) {
   return out;
 }
 
-template <int BN, int BK>
+// fp8 X images ([32 points][RB bytes], RB = BK): chunk c of row r at c ^ pm_swz8(r), so that the transposed reads of a
+// 32-lane half (16 rows x one chunk, two 8-byte halves) hit 64 distinct banks for RB = 64 / 128 / 256
+template <int RB>
+__device__ __forceinline__ int pm_swz8(int r) {
+  static_assert(RB == 64 || RB == 128 || RB == 256, "fp8 pm image row width");
+  return (r / (256 / RB)) & (RB / 16 - 1);
+}
+// fragment of 16 features x 8 points from an fp8 image: ds_read_b64_tr_b8 (per 16-lane group, lane 2q+p supplies row q,
+// bytes 8p..8p+7 of a 16-byte chunk; lane i receives column i of the 8 rows, row q in byte q: tools/probes/probe_tr8.hip)
+// gives lane (g, i) points 8g..8g+7 of feature f0 + i, widened to bf16 exactly (e4m3 fits bf16) for the bf16 MFMA
+template <int RB>
+__device__ __forceinline__ f4 pm_frag8(const char* img, int f0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 1, p = i & 1;
+  const int r = 8 * g + q;
+  const char* a = img + r * RB + 16 * ((f0 / 16) ^ pm_swz8<RB>(r)) + 8 * p;
+  typedef int i32x2 __attribute__((ext_vector_type(2)));
+  const i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) i32x2*)(a));
+  f4 out;
+  out.x = __builtin_bit_cast(float, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.x, 1.0f, false));
+  out.y = __builtin_bit_cast(float, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.x, 1.0f, true));
+  out.z = __builtin_bit_cast(float, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.y, 1.0f, false));
+  out.w = __builtin_bit_cast(float, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.y, 1.0f, true));
+  return out;
+}
+
+template <int BN, int BK, bool X8>
 __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S, int64_t Npad, float* __restrict__ slab,
                                            int64_t slab_elems, char* smem) {
   constexpr int WN = BN / 64, WK0 = 8 / WN, WK = (BK / 16 < WK0) ? BK / 16 : WK0, KTW = BK / WK / 16;
   static_assert(KTW >= 1 && WN * WK <= 8, "dW wave tiling");
-  constexpr int AB = PM_SPTS * BN * 2, XB = PM_SPTS * BK * 2;  // image bytes
-  constexpr int NI = (AB + XB) / 1024, PW = (NI + 7) / 8;      // DMA wave-instructions per stage / per wave
+  constexpr int XEB = X8 ? 1 : 2, RBX = BK * XEB;             // X element bytes, X image row bytes
+  constexpr int AB = PM_SPTS * BN * 2, XB = PM_SPTS * RBX;    // image bytes
+  constexpr int NI = (AB + XB + 1023) / 1024, PW = (NI + 7) / 8;  // DMA wave-instructions per stage / per wave
+  static_assert((AB + XB) % 1024 == 0, "pm dW images: whole DMA wave-instructions");
   static_assert(PW * 8 * 1024 <= DW_STAGE_BYTES, "pm dW stage");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1757,30 +1883,37 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
   const bool mma_wave = wave < WN * WK;
   const int64_t nst = Npad / PM_SPTS;
   const int64_t st_lo = nst * s / S, st_hi = nst * (s + 1) / S;
-  // this lane's DMA source per wave-instruction and its per-stage advance (32 points of its section)
-  const bf16_t* src[PW];
+  // this lane's DMA source per wave-instruction and its per-stage advance (32 points of its section), in bytes
+  const char* src[PW];
   int64_t adv[PW];
+  const int x0b = J.x0_u8 ? 1 : 2, x1b = J.x1_u8 ? 1 : 2;  // == XEB for the section(s) this tile reads
 #pragma unroll
   for (int i = 0; i < PW; ++i) {
     const int ii = 8 * i + wave;
     const int b = (ii < NI ? ii : 0) * 1024 + lane * 16;
     if (b < AB) {
       const int r = b / (2 * BN), c = ((b % (2 * BN)) / 16) ^ pm_swz<2 * BN>(r);
-      src[i] = (const bf16_t*)J.A + (int64_t)r * J.a_ld + 8 * (c < J.a_chunks ? c : 0);
-      adv[i] = (int64_t)PM_SPTS * J.a_ld;
-    } else {
-      const int bx = b - AB, r = bx / (2 * BK), c = ((bx % (2 * BK)) / 16) ^ pm_swz<2 * BK>(r);
-      const int j = k0 + 8 * c;  // virtual column
+      src[i] = (const char*)J.A + ((int64_t)r * J.a_ld + 8 * (c < J.a_chunks ? c : 0)) * 2;
+      adv[i] = (int64_t)PM_SPTS * J.a_ld * 2;
+    } else if (b < AB + XB) {
+      const int bx = b - AB, r = bx / RBX;
+      int c;
+      if constexpr (X8) c = ((bx % RBX) / 16) ^ pm_swz8<RBX>(r);
+      else c = ((bx % RBX) / 16) ^ pm_swz<RBX>(r);
+      const int j = k0 + (16 / XEB) * c;  // virtual column
       if (j < J.x0p) {
-        src[i] = (const bf16_t*)J.X0 + (int64_t)r * J.x0_ld + j;
-        adv[i] = (int64_t)PM_SPTS * J.x0_ld;
+        src[i] = (const char*)J.X0 + ((int64_t)r * J.x0_ld + j) * x0b;
+        adv[i] = (int64_t)PM_SPTS * J.x0_ld * x0b;
       } else if (j - J.x0p < J.x1_ld && J.X1) {
-        src[i] = (const bf16_t*)J.X1 + (int64_t)r * J.x1_ld + (j - J.x0p);
-        adv[i] = (int64_t)PM_SPTS * J.x1_ld;
+        src[i] = (const char*)J.X1 + ((int64_t)r * J.x1_ld + (j - J.x0p)) * x1b;
+        adv[i] = (int64_t)PM_SPTS * J.x1_ld * x1b;
       } else {  // past the virtual width: any valid address (never stored)
-        src[i] = (const bf16_t*)J.X0 + (int64_t)r * J.x0_ld;
-        adv[i] = (int64_t)PM_SPTS * J.x0_ld;
+        src[i] = (const char*)J.X0 + (int64_t)r * J.x0_ld * x0b;
+        adv[i] = (int64_t)PM_SPTS * J.x0_ld * x0b;
       }
+    } else {  // padding of the last wave-instruction: a valid source into unused LDS
+      src[i] = (const char*)J.A;
+      adv[i] = 0;
     }
   }
   auto issue = [&](int64_t st) {
@@ -1806,7 +1939,7 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
     if (st_lo + i < st_hi) issue(st_lo + i);
   for (int64_t st = st_lo; st < st_hi; ++st) {
     const int64_t ahead = st_hi - 1 - st;
-    static_assert(PM_STAGES >= 3 && PM_STAGES <= 5, "wait ladder below");
+    static_assert(PM_STAGES >= 2 && PM_STAGES <= 5, "wait ladder below");
     if (ahead >= PM_STAGES - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (PM_STAGES - 2)) : "memory");
     else if (PM_STAGES == 5 && ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * 2) : "memory");
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
@@ -1824,7 +1957,10 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
       for (int q0 = 0; q0 < KTW; q0 += QG) {
         f4 b[QG];
 #pragma unroll
-        for (int q = 0; q < QG; ++q) b[q] = pm_frag<2 * BK>(buf + AB, (wk * KTW + q0 + q) * 16, lane);
+        for (int q = 0; q < QG; ++q) {
+          if constexpr (X8) b[q] = pm_frag8<RBX>(buf + AB, (wk * KTW + q0 + q) * 16, lane);
+          else b[q] = pm_frag<RBX>(buf + AB, (wk * KTW + q0 + q) * 16, lane);
+        }
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
@@ -2014,18 +2150,25 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   const int bk = kt < J.k_full ? BKMAX : J.bk_tail;
   const int64_t se = jobs.slab_elems;
   if constexpr (Cfg<T>::PM) {
-    if (J.bn == 256) {
-      if (bk == 256) dw_tile_pm<256, 256>(J, k0, s, S, Npad, slab, se, smem);
-      else if (bk == 128) dw_tile_pm<256, 128>(J, k0, s, S, Npad, slab, se, smem);
-      else dw_tile_pm<256, 64>(J, k0, s, S, Npad, slab, se, smem);
-    } else if (J.bn == 128) {
-      if (bk == 256) dw_tile_pm<128, 256>(J, k0, s, S, Npad, slab, se, smem);
-      else if (bk == 128) dw_tile_pm<128, 128>(J, k0, s, S, Npad, slab, se, smem);
-      else dw_tile_pm<128, 64>(J, k0, s, S, Npad, slab, se, smem);
-    } else {
-      if (bk == 256) dw_tile_pm<64, 256>(J, k0, s, S, Npad, slab, se, smem);
-      else dw_tile_pm<64, 128>(J, k0, s, S, Npad, slab, se, smem);
-    }
+    // the tile's X format: fp8 if its columns come from an fp8 section (a k-tile never mixes formats: host check)
+    const bool x8 = (k0 < J.x0p) ? J.x0_u8 : J.x1_u8;
+    auto run = [&](auto xc) {
+      constexpr bool X8 = decltype(xc)::value;
+      if (J.bn == 256) {
+        if (bk == 256) dw_tile_pm<256, 256, X8>(J, k0, s, S, Npad, slab, se, smem);
+        else if (bk == 128) dw_tile_pm<256, 128, X8>(J, k0, s, S, Npad, slab, se, smem);
+        else dw_tile_pm<256, 64, X8>(J, k0, s, S, Npad, slab, se, smem);
+      } else if (J.bn == 128) {
+        if (bk == 256) dw_tile_pm<128, 256, X8>(J, k0, s, S, Npad, slab, se, smem);
+        else if (bk == 128) dw_tile_pm<128, 128, X8>(J, k0, s, S, Npad, slab, se, smem);
+        else dw_tile_pm<128, 64, X8>(J, k0, s, S, Npad, slab, se, smem);
+      } else {
+        if (bk == 256) dw_tile_pm<64, 256, X8>(J, k0, s, S, Npad, slab, se, smem);
+        else dw_tile_pm<64, 128, X8>(J, k0, s, S, Npad, slab, se, smem);
+      }
+    };
+    if (x8) run(std::integral_constant<bool, true>{});
+    else run(std::integral_constant<bool, false>{});
   } else if constexpr (is_x3<T>) {
     if (J.bn == 256) {
       if (bk == 128) dw_tile_x3<256, 128>(J, k0, s, S, Npad, slab, se, smem);
@@ -2167,12 +2310,30 @@ static void for_each_dw_job(const MlpLayout& L, bool pm, F&& f) {
   f(DwSpec{GR.du, L.cdim, 16, 0, SR.c, L.hdir, HC, -1, 0, 0, h + 6});                    // color_layer.2
 }
 
+// X0's padded width in a point-major tile: whole 16-byte chunks (8 bf16 / 16 fp8 columns)
+static int dw_x0p(const MlpLayout& L, bool pm, const DwSpec& sp) {
+  if (!pm) return sp.x0_rows;
+  int es = 2;
+  pm_sec_bytes(L.L, 128, sp.x0, &es);
+  const int q = es == 1 ? 16 : 8;
+  return (sp.x0_rows + q - 1) / q * q;
+}
+
 static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void* gradbuf, int64_t Npad,
                           float* const* grads, DwJobs& D) {
   const size_t es = elem_size(prec);
   const bool pm = prec_pm(prec);
   const int64_t ld = pm ? Npad : row_ld(Npad, es);
   auto srow = [&](int64_t r) { return r < 0 ? nullptr : (const void*)((const char*)saved + r * ld * es); };
+  // point-major (bf16): sections at byte offsets, some in fp8 (pm_save)
+  auto psec = [&](int64_t r, int* u8) -> const void* {
+    *u8 = 0;
+    if (r < 0) return nullptr;
+    int b = 2;
+    const int64_t off = pm_sec_bytes(L.L, Npad, r, &b);
+    *u8 = b == 1;
+    return (const void*)((const char*)saved + off);
+  };
   auto grow = [&](int64_t r) { return (const void*)((const char*)gradbuf + r * ld * es); };
   D.n = 0;
   D.total_tiles = 0;
@@ -2180,12 +2341,20 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
   for_each_dw_job(L, pm, [&](const DwSpec& sp) {
     DwJob& j = D.j[D.n++];
     j.A = grow(sp.arow); j.a_rows = sp.a_rows;
-    j.X0 = srow(sp.x0); j.x0_rows = sp.x0_rows; j.X1 = srow(sp.x1); j.x1_rows = sp.x1_rows;
+    j.x0_u8 = j.x1_u8 = 0;
+    if (pm) {
+      j.X0 = psec(sp.x0, &j.x0_u8);
+      j.X1 = psec(sp.x1, &j.x1_u8);
+    } else {
+      j.X0 = srow(sp.x0);
+      j.X1 = srow(sp.x1);
+    }
+    j.x0_rows = sp.x0_rows; j.x1_rows = sp.x1_rows;
     j.ktot = sp.x0_rows + sp.x1_rows;
     j.a_ld = sp.a_w; j.x0_ld = sp.x0_w; j.x1_ld = sp.x1_w;
     if (pm) j.A = (const char*)j.A + (int64_t)sp.a_col * es;
     j.a_chunks = (sp.a_w - sp.a_col) / 8;
-    j.x0p = pm ? (sp.x0_rows + 7) / 8 * 8 : sp.x0_rows;
+    j.x0p = dw_x0p(L, pm, sp);
     j.ktot_v = j.x0p + sp.x1_rows;
     j.bn = dw_bn(sp.a_rows);
     dw_ktiles(j.ktot_v, j.bn, prec, &j.k_full, &j.bk_tail, &j.k_tiles);
@@ -2204,7 +2373,7 @@ static int64_t dw_slab_elems_for(const MlpLayout& L, int prec, int* total_tiles)
   const bool pm = prec_pm(prec);
   for_each_dw_job(L, pm, [&](const DwSpec& sp) {
     const int ktot = sp.x0_rows + sp.x1_rows;
-    const int ktot_v = (pm ? (sp.x0_rows + 7) / 8 * 8 : sp.x0_rows) + sp.x1_rows;
+    const int ktot_v = dw_x0p(L, pm, sp) + sp.x1_rows;
     e += (int64_t)sp.a_rows * (ktot + 1);
     int kf, bt, kt;
     dw_ktiles(ktot_v, dw_bn(sp.a_rows), prec, &kf, &bt, &kt);
@@ -2259,6 +2428,9 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   if (!dw && !red) return 0;
   DwJobs D;
   build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D);
+  for (int i = 0; i < D.n; ++i)  // a point-major k-tile reads one X format: mixed sections must split at a tile edge
+    YN_CHECK(!D.j[i].X1 || D.j[i].x0_u8 == D.j[i].x1_u8 || D.j[i].x0p % dw_bkmax(prec) == 0,
+             "mlp_backward: dW job %d mixes fp8 and bf16 columns inside a tile", i);
   const int S = dw_splits(D.total_tiles, Npad / dw_stage_pts(prec));
   if (dw) {
     hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)(D.total_tiles * S)), dim3(DW_THREADS), 0, st, D, Npad, S,

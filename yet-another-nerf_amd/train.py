@@ -272,6 +272,13 @@ class NeRFTrainer:
                                                  _p(noise), _p(ps.g_feats), None, None, R, P, C, _p(ps.g_sigma),
                                                  _p(ps.g_rgb), st), "yanerf_composite_backward")
             out["sq_coarse" if k == 0 else "sq_fine"] = ps.sq
+            if k == 0 and self.overlap == "early" and not self.kernel_probes:
+                # the coarse pass's loss and gradients are complete here and nothing of the fine pass depends on them:
+                # its MLP backward (dX: MFMA-bound, dW: bandwidth-bound) runs on the side stream beside the refinement
+                # and the fine forward (MFMA-bound) instead of after it
+                self.side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(self.side):
+                    self._mlp_backward(0, ctypes.c_void_p(self.side.cuda_stream), self.side)
         if self.kernel_probes:
             # timing probe mode (bench.py's per-kernel roofline): every MLP backward kernel alone on the stream, in the
             # order dX, dW, slab reduce; the result is identical to the other schedules
@@ -281,6 +288,9 @@ class NeRFTrainer:
         elif self.side is None:
             self._mlp_backward(1, st)
             self._mlp_backward(0, st)
+        elif self.overlap == "early":
+            self._mlp_backward(1, st)
+            torch.cuda.current_stream().wait_stream(self.side)
         elif self.overlap == "split":
             self._mlp_backward(0, st, phase=1)
             self.side.wait_stream(torch.cuda.current_stream())

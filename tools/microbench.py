@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Per-kernel timing of the MLP kernels at the Lego fine-pass size (4096 rays x 192 points), interleaved A/B in
 one process (HIP events on the launch stream). Variants: forward with / without the saved-activation stream,
-backward (dX + dW + reduce). Development tool; prints one JSON line."""
+backward (dX + dW + reduce) and its three kernels alone. Development tool; prints one JSON line."""
 import ctypes
 import json
 import sys
@@ -51,7 +51,12 @@ def main(R=4096, P=192, reps=10):
             _C.check(L.yanerf_mlp_backward(ctypes.byref(d), spec.precision, P_(packed), P_(saved), P_(rgb), P_(gs),
                                            P_(gr), R, P, gp, P_(ws), st), "bwd")
 
-        variants = {"fwd_train": lambda: fwd(True), "fwd_infer": lambda: fwd(False), "bwd": bwd}
+        def bwd_phase(ph):
+            _C.check(L.yanerf_mlp_backward_phase(ctypes.byref(d), spec.precision, P_(packed), P_(saved), P_(rgb),
+                                                 P_(gs), P_(gr), R, P, gp, P_(ws), ph, st), "bwd_phase")
+
+        variants = {"fwd_train": lambda: fwd(True), "fwd_infer": lambda: fwd(False), "bwd": bwd,
+                    "bwd_dx": lambda: bwd_phase(1), "bwd_dw": lambda: bwd_phase(4), "bwd_reduce": lambda: bwd_phase(8)}
         times = {k: [] for k in variants}
         for k in variants:  # warm
             variants[k]()
@@ -68,7 +73,7 @@ def main(R=4096, P=192, reps=10):
         for k, evs in times.items():
             ms = sorted(a.elapsed_time(b) for a, b in evs)
             med = ms[len(ms) // 2]
-            fl = flop * (2.0 if k == "bwd" else 1.0)
+            fl = flop * (2.0 if k == "bwd" else 1.0 if k.startswith("fwd") or k in ("bwd_dx", "bwd_dw") else 0.0)
             res[f"{prec}_{k}"] = {"ms": round(med, 4), "tflops": round(fl / med / 1e9, 1)}
     print(json.dumps(res))
 

@@ -240,6 +240,55 @@ static int64_t pm_sec_bytes(int L, int64_t Npad, int64_t r0, int* es) {
   *es = PM_HB;
   return PS.c;  // r0 == SR.c
 }
+#ifndef YANERF_BF16_G8
+#define YANERF_BF16_G8 1
+#endif
+constexpr int PM_GB = YANERF_BF16_G8 ? 1 : 2;  // bytes per dZ / dY / dZc element in the bf16 backward workspace
+// bf16 backward workspace (point-major): byte offsets of the gradient sections, the dU section (bf16: du_j at column j,
+// dsigma at PM_DSIG) and the per-(section, 128-point tile) fp8 scales (float; sections dZ_0..dZ_{L-1}, dY, dZc)
+struct PmGrad {
+  int64_t dz0, dy, dzc, du, scale, total;
+};
+__host__ __device__ inline PmGrad pm_grad(int L, int64_t Npad) {
+  PmGrad g;
+  int64_t o = 0;
+  g.dz0 = o; o += (int64_t)PM_GB * 256 * L * Npad;
+  g.dy = o; o += (int64_t)PM_GB * 256 * Npad;
+  g.dzc = o; o += (int64_t)PM_GB * HC * Npad;
+  g.du = o; o += 2LL * 16 * Npad;
+  g.scale = o; o += 4LL * (L + 2) * (Npad / 128);
+  g.total = (o + 255) / 256 * 256;
+  return g;
+}
+// byte offset, element bytes and scale array (or null) of the gradient section starting at GradRows row r0
+static int64_t pm_grad_sec(int L, int64_t Npad, int64_t r0, int* es, int64_t* scale_off) {
+  const GradRows GR = grad_rows(L, true);
+  const PmGrad PG = pm_grad(L, Npad);
+  *es = PM_GB;
+  *scale_off = -1;
+  int sec;
+  int64_t off;
+  if (r0 >= GR.dz0 && r0 < GR.dyx) {
+    sec = (int)((r0 - GR.dz0) / 256);
+    off = PG.dz0 + (int64_t)sec * PM_GB * 256 * Npad;
+  } else if (r0 == GR.dyx) {
+    sec = L;
+    off = PG.dy;
+  } else if (r0 == GR.dzc) {
+    sec = L + 1;
+    off = PG.dzc;
+  } else {  // dU (bf16, unscaled)
+    *es = 2;
+    return PG.du;
+  }
+  if (YANERF_BF16_G8) *scale_off = PG.scale + 4LL * sec * (Npad / 128);
+  return off;
+}
+// backward workspace bytes before the dW slabs
+static int64_t grad_t_bytes(int L, int64_t Npad, size_t es, bool pm) {
+  if (pm) return pm_grad(L, Npad).total;
+  return grad_rows(L).rows * row_ld(Npad, es) * (int64_t)es;
+}
 static int64_t saved_t_bytes(int L, int64_t Npad, size_t es, bool pm) {
   if (pm) return pm_save(L, Npad).total;
   return saved_rows(L).rows * row_ld(Npad, es) * (int64_t)es;
@@ -1058,20 +1107,27 @@ __device__ __forceinline__ void copy_tile_pm(const typename Cfg<T>::lds_t* act, 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t fp8x4_from_bf16(uint32_t w0, uint32_t w1) {
-  const u16x2 cap = {0x43E0, 0x43E0};  // 448.0 in bf16
-  const u16x2 a = __builtin_elementwise_min(__builtin_bit_cast(u16x2, w0), cap);
-  const u16x2 b = __builtin_elementwise_min(__builtin_bit_cast(u16x2, w1), cap);
-  i16x2 r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(i16x2{0, 0}, __builtin_bit_cast(bf16x2, a), 1.0f, false);
-  r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, __builtin_bit_cast(bf16x2, b), 1.0f, true);
+// four bf16 (two packed words) -> four fp8 e4m3 of value / scale (v_cvt_scalef32_pk_fp8_bf16 divides by its scale
+// operand and v_cvt_scalef32_pk_bf16_fp8 multiplies: tools/probes/probe_fp8_scale.hip). CLAMP: the inputs are
+// non-negative and may exceed 448 (integer min on the bf16 bits); otherwise the caller's scale keeps |value| < 448.
+template <bool CLAMP>
+__device__ __forceinline__ uint32_t fp8x4_from_bf16(uint32_t w0, uint32_t w1, float scale) {
+  if constexpr (CLAMP) {
+    const u16x2 cap = {0x43E0, 0x43E0};  // 448.0 in bf16
+    w0 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, w0), cap));
+    w1 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, w1), cap));
+  }
+  i16x2 r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(i16x2{0, 0}, __builtin_bit_cast(bf16x2, w0), scale, false);
+  r = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(r, __builtin_bit_cast(bf16x2, w1), scale, true);
   return __builtin_bit_cast(uint32_t, r);
 }
-template <typename T, int NTHR, int W>
-__device__ __forceinline__ void copy_tile_pm_fp8(const typename Cfg<T>::lds_t* act, int col0, uint8_t* dst, int tid) {
+template <typename T, int NTHR, int W, bool CLAMP = true, int GMAX = 4>
+__device__ __forceinline__ void copy_tile_pm_fp8(const typename Cfg<T>::lds_t* act, int col0, uint8_t* dst, int tid,
+                                                 float scale = 1.0f) {
   static_assert(sizeof(typename Cfg<T>::lds_t) == 2 && !is_x3<T>, "fp8 save: bf16 tiles");
   constexpr int M = Cfg<T>::M, OPR = W / 16, TOT = M * OPR, IT = TOT / NTHR;
   static_assert(TOT % NTHR == 0 && NTHR % OPR == 0, "copy_tile_pm_fp8: whole chunks / rows per pass");
-  constexpr int GRP = IT < 4 ? IT : 4;
+  constexpr int GRP = IT < GMAX ? IT : GMAX;  // output chunks in flight per lane (8 + 4 VGPRs each)
   int t = tid;
   asm volatile("" : "+v"(t));
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
@@ -1089,12 +1145,14 @@ __device__ __forceinline__ void copy_tile_pm_fp8(const typename Cfg<T>::lds_t* a
     }
 #pragma unroll
     for (int i = 0; i < GRP; ++i) {
-      const u32x4 out = {fp8x4_from_bf16(__float_as_uint(lo[i].x), __float_as_uint(lo[i].y)),
-                         fp8x4_from_bf16(__float_as_uint(lo[i].z), __float_as_uint(lo[i].w)),
-                         fp8x4_from_bf16(__float_as_uint(hi[i].x), __float_as_uint(hi[i].y)),
-                         fp8x4_from_bf16(__float_as_uint(hi[i].z), __float_as_uint(hi[i].w))};
-      // offset in the VGPR offset, soffset = 0 (the wide-store hazard note at copy_tile_pm)
+      const u32x4 out = {fp8x4_from_bf16<CLAMP>(__float_as_uint(lo[i].x), __float_as_uint(lo[i].y), scale),
+                         fp8x4_from_bf16<CLAMP>(__float_as_uint(lo[i].z), __float_as_uint(lo[i].w), scale),
+                         fp8x4_from_bf16<CLAMP>(__float_as_uint(hi[i].x), __float_as_uint(hi[i].y), scale),
+                         fp8x4_from_bf16<CLAMP>(__float_as_uint(hi[i].z), __float_as_uint(hi[i].w), scale)};
+      // offset in the VGPR offset, soffset = 0 (the wide-store hazard note at copy_tile_pm); the nop keeps the next
+      // group's LDS reads (which reuse these VGPRs) one instruction away from the store
       __builtin_amdgcn_raw_buffer_store_b128(out, rs, goff + (uint32_t)((i0 + i) * NTHR * 16), 0, 0);
+      asm volatile("s_nop 0" ::: "memory");
     }
   }
 }
@@ -1103,6 +1161,49 @@ template <typename T, int NTHR, int W>
 __device__ __forceinline__ void save_relu_pm(const typename Cfg<T>::lds_t* act, int col0, char* dst, int tid) {
   if constexpr (YANERF_BF16_A8) copy_tile_pm_fp8<T, NTHR, W>(act, col0, (uint8_t*)dst, tid);
   else copy_tile_pm<T, NTHR, W>(act, col0, (typename Cfg<T>::st_t*)dst, tid);
+}
+
+// fp8 gradient rows (YANERF_BF16_G8): the dX kernel's pre-activation gradients dZ_l, dY and dZc are the dW kernel's A
+// operands only. Each leaves a tile as fp8 e4m3 of value / s with one power-of-two s per (section, 128-point tile),
+// chosen so the tile's largest |value| lands in [128, 256) (below e4m3's 448 after the bf16 rounding of the LDS copy);
+// s goes to a small scale array beside the rows and the dW tile widens the fragments with it (exact).
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// running |max| of packed bf16 tile values as two u16 maxima of the magnitude bits (one VGPR, two VALU per chunk)
+struct G8Max {
+  u16x2 m = {0, 0};
+  template <typename T> __device__ __forceinline__ void add(const Pk<T>& h) {
+    if constexpr (std::is_same<T, bf16_t>::value) {
+      m = __builtin_elementwise_max(m, __builtin_bit_cast(u16x2, h.w0 & 0x7fff7fffu));
+      m = __builtin_elementwise_max(m, __builtin_bit_cast(u16x2, h.w1 & 0x7fff7fffu));
+    }
+  }
+  __device__ __forceinline__ float value() const {
+    const uint32_t b = m.x > m.y ? m.x : m.y;
+    return __uint_as_float(b << 16);
+  }
+};
+__device__ __forceinline__ float g8_scale(float amax) {
+  const uint32_t e = (__float_as_uint(amax) >> 23) & 0xffu;
+  return e <= 7u ? 1.0f : __uint_as_float((e - 7u) << 23);
+}
+// the gradient tile's save: `red` holds each wave's |max| of the section (written before the last barrier)
+template <typename T, int NTHR, int W>
+__device__ __forceinline__ void save_grad_pm(const typename Cfg<T>::lds_t* act, char* dst, float* scale_out,
+                                             const float* red, int waves, int tid) {
+  if constexpr (YANERF_BF16_G8) {
+    float amax = red[0];
+    for (int w = 1; w < waves; ++w) amax = fmaxf(amax, red[w]);
+    const float sc = g8_scale(amax);
+    if (tid == 0) *scale_out = sc;
+    // two chunks in flight: the dX trunk step copies while the next layer's weight ring is live
+    copy_tile_pm_fp8<T, NTHR, W, false, 2>(act, 0, (uint8_t*)dst, tid, sc);
+  } else {
+    copy_tile_pm<T, NTHR, W>(act, 0, (typename Cfg<T>::st_t*)dst, tid);
+  }
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global stores (the
@@ -1361,6 +1462,20 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
   constexpr bool PM = Cfg<T>::PM;
   constexpr int NTHR = WAVES * 64;
   const GradRows GR = grad_rows(lay.L, PM);
+  // point-major: byte sections (pm_grad); per-wave |max| of each gradient section for its fp8 scale in LDS slots past
+  // the colour-output weights (PE columns of row 16), two sets used alternately: a set is rewritten only after the
+  // barrier that follows the copy reading it
+  [[maybe_unused]] char* const gb = (char*)grad;
+  [[maybe_unused]] const PmGrad PG = pm_grad(lay.L, Npad);
+  [[maybe_unused]] float* const g8red = (float*)(act + 16 * ROW + PE_COL);
+  [[maybe_unused]] float* const g8scl = (float*)(gb + PG.scale) + blockIdx.x;
+  [[maybe_unused]] const int64_t ntile = Npad / M;
+  auto g8_note = [&](int set, float amax) {  // this wave's |max| of the section being formed
+    if constexpr (PM && YANERF_BF16_G8) {
+      amax = wave_max(amax);
+      if (lane == 0) g8red[8 * set + wave] = amax;
+    }
+  };
   const int mt_ = tid / TPP, q = tid % TPP;
   const int64_t p = p0 + mt_;
   const bool valid = p < N;
@@ -1376,8 +1491,9 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
   }
   if (q == 0) {
     if constexpr (PM) {
-      for (int j = 0; j < cd; ++j) grad[GR.du * Npad + p * 16 + j] = to_st<T>(du[j]);
-      grad[GR.du * Npad + p * 16 + PM_DSIG] = to_st<T>(gs);
+      ST* gdu = (ST*)(gb + PG.du) + p * 16;
+      for (int j = 0; j < cd; ++j) gdu[j] = to_st<T>(du[j]);
+      gdu[PM_DSIG] = to_st<T>(gs);
     } else {
       for (int j = 0; j < cd; ++j) grad[(GR.du + j) * ld + p] = to_st<T>(du[j]);
       grad[(GR.dyx + 256) * ld + p] = to_st<T>(gs);
@@ -1404,6 +1520,9 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
     // would put it in scratch); the colour-output sum runs over j < cd with the reference's order, unrolled to CMAX
     // with a predicate, and every 16-byte chunk of the row goes to LDS in one store
     constexpr int EPC = Cfg<T>::EPC;
+    static_assert(16 * ROW + PE_COL + 16 * (int)sizeof(float) / (int)sizeof(LT) <= M * ROW &&
+                      (CMAX * HC) / WFPR <= 16, "fp8 scale slots after the colour-output weights");
+    float amax = 0.0f;
     lds_barrier();
 #pragma unroll
     for (int t = 0; t < TT; ++t)
@@ -1435,9 +1554,11 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
           dz[e] = on ? dc[e] : 0.0f;
           if constexpr ((YANERF_ABLATE & 64) != 0) dz[e] = (float)c;
           if constexpr (!PM) grad[(GR.dzc + c) * ld + p] = to_st<T>(dz[e]);
+          amax = fmaxf(amax, fabsf(dz[e]));
         }
         lds_put_chunk<T>(act, mt_, (CPT * q + 16 * t + c0) / EPC, dz);
       }
+    g8_note(0, amax);  // dZc: set 0
   }
   lds_barrier();
   f4 acc[NT][MT];
@@ -1448,8 +1569,10 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
   ring_fill<T, NT>(ring, Wt + lay.wintT_off, wpl, 256, nrow0, 256 / KB, lane);
   // point-major gradients leave the LDS tile after the GEMM that reads them (and its next-ring loads): see the
   // forward's trunk loop on the shared, in-order vmcnt
-  if constexpr (PM) copy_tile_pm<T, NTHR, HC>(act, 0, grad + GR.dzc * Npad + p0 * HC, tid);
+  if constexpr (PM)
+    save_grad_pm<T, NTHR, HC>(act, gb + PG.dzc + p0 * HC * PM_GB, g8scl + (lay.L + 1) * ntile, g8red, WAVES, tid);
   lds_barrier();
+  G8Max gmax;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int n = nrow0 + 16 * nt + 4 * g;
@@ -1458,12 +1581,14 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
       const int m = 16 * mt + li;
       f4 v = acc[nt][mt];
       const Pk<T> h = pk_make<T>(v);
+      if constexpr (PM && YANERF_BF16_G8) gmax.add(h);
       pk_lds<T>(act, m, n, h);
       if constexpr (!PM)
         pk_store_rows_b<T>((grad + (GR.dyx + nrow0 + 16 * nt) * ld + p0),
                              soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
     }
   }
+  g8_note(1, gmax.value());  // dY: set 1
   lds_barrier();
   // ---- dH_{L-1} = Wint^T dY + w_d (x) dsigma ; dZ_{L-1} = dH * [H_{L-1} > 0], then trunk layer l -> l-1.
   // One step: the GEMM with the transposed weights (Wint^T from the heads, else layer l's), then the masked epilogue
@@ -1479,11 +1604,16 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
       bits[w] = masks[((((int64_t)hl * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane];
     gemm_lds<T, NT, MT>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring);
     if (l - 1 >= 1) ring_fill<T, NT>(ring, Wt + lay.wt_off[l - 1], wpl, 256, nrow0, 256 / KB, lane);
+    // fp8 scale sets: dZc 0, dY 1, then dZ_{L-1}, dZ_{L-2}, ... alternate from set 0
     if constexpr (PM && !(YANERF_ABLATE & 128)) {  // the GEMM's input: dY (from the heads) or dZ_l
-      if constexpr (HEAD) copy_tile_pm<T, NTHR, 256>(act, 0, grad + GR.dyx * Npad + p0 * 256, tid);
-      else copy_tile_pm<T, NTHR, 256>(act, 0, grad + (GR.dz0 + 256LL * l) * Npad + p0 * 256, tid);
+      if constexpr (HEAD)
+        save_grad_pm<T, NTHR, 256>(act, gb + PG.dy + p0 * 256 * PM_GB, g8scl + lay.L * ntile, g8red + 8, WAVES, tid);
+      else
+        save_grad_pm<T, NTHR, 256>(act, gb + PG.dz0 + ((int64_t)l * Npad + p0) * 256 * PM_GB, g8scl + l * ntile,
+                                   g8red + 8 * ((lay.L + 1 - l) & 1), WAVES, tid);
     }
     lds_barrier();
+    G8Max gmax;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int n = nrow0 + 16 * nt + 4 * g;
@@ -1499,17 +1629,20 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
         }
         // ReLU mask of H_{hl}: this lane's own bits of this tile (packed by the forward)
         const Pk<T> h = pk_make<T>(apply_mask_tile<T, MW>(v, bits, nt * MT + mt));
+        if constexpr (PM && YANERF_BF16_G8) gmax.add(h);
         pk_lds<T>(act, m, n, h);
         if constexpr (!PM)
           pk_store_rows_b<T>((grad + (GR.dz0 + 256LL * hl + nrow0 + 16 * nt) * ld + p0),
                              soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
       }
     }
+    g8_note((lay.L + 1 - hl) & 1, gmax.value());  // dZ_hl
     lds_barrier();
   };
   trunk_step(std::integral_constant<bool, true>{}, lay.L);
   for (int l = lay.L - 1; l >= 1; --l) trunk_step(std::integral_constant<bool, false>{}, l);
-  if constexpr (PM && !(YANERF_ABLATE & 128)) copy_tile_pm<T, NTHR, 256>(act, 0, grad + GR.dz0 * Npad + p0 * 256, tid);
+  if constexpr (PM && !(YANERF_ABLATE & 128))
+    save_grad_pm<T, NTHR, 256>(act, gb + PG.dz0 + p0 * 256 * PM_GB, g8scl, g8red + 8 * ((lay.L + 1) & 1), WAVES, tid);
 }
 
 // ============================================================================================ backward dW
@@ -1541,6 +1674,8 @@ struct DwJob {
   // padded to x0p (a multiple of 8), then X1's (ktot_v = x0p + x1_rows); k-tiles are laid over ktot_v
   int a_ld, a_chunks, x0_ld, x1_ld, x0p, ktot_v;
   int x0_u8, x1_u8;  // X0 / X1 stored as fp8 e4m3 (YANERF_BF16_A8: the post-ReLU sections); a k-tile is one format
+  int a_u8;          // A stored as fp8 e4m3 of value / scale (YANERF_BF16_G8: dZ_l, dY, dZc; not dU)
+  const float* a_scale;  // A's decode scale per 128-point tile
 };
 constexpr int kMaxDwJobs = MAXL + 4;
 struct DwJobs {
@@ -1822,6 +1957,10 @@ constexpr int PM_SPTS = 32;  // points per dW stage
 #define YANERF_PM_STAGES 4
 #endif
 constexpr int PM_STAGES = YANERF_PM_STAGES;  // LDS-DMA ring depth of the point-major (bf16) dW tile
+// fp8 gradient scales of one split (one per 128-point tile), staged in LDS after the ring at the tile's start: a load
+// per stage would be a vector load (the DMA intrinsics keep the compiler from proving the scales read-only for a
+// scalar load), and waiting for it would drain the in-order DMA counter
+constexpr int PM_SCALES = 512;
 typedef short s4v __attribute__((ext_vector_type(4)));
 // fragment of 16 features x 8 points (points 8g..8g+7 of the stage for lane group g) from an image with ROWB-byte rows
 template <int ROWB>
@@ -1852,27 +1991,29 @@ __device__ __forceinline__ int pm_swz8(int r) {
 // bytes 8p..8p+7 of a 16-byte chunk; lane i receives column i of the 8 rows, row q in byte q: tools/probes/probe_tr8.hip)
 // gives lane (g, i) points 8g..8g+7 of feature f0 + i, widened to bf16 exactly (e4m3 fits bf16) for the bf16 MFMA
 template <int RB>
-__device__ __forceinline__ f4 pm_frag8(const char* img, int f0, int lane) {
+__device__ __forceinline__ f4 pm_frag8(const char* img, int f0, int lane, float scale = 1.0f) {
   const int g = lane >> 4, i = lane & 15, q = i >> 1, p = i & 1;
   const int r = 8 * g + q;
   const char* a = img + r * RB + 16 * ((f0 / 16) ^ pm_swz8<RB>(r)) + 8 * p;
   typedef int i32x2 __attribute__((ext_vector_type(2)));
   const i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) i32x2*)(a));
   f4 out;
-  out.x = __builtin_bit_cast(float, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.x, 1.0f, false));
-  out.y = __builtin_bit_cast(float, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.x, 1.0f, true));
-  out.z = __builtin_bit_cast(float, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.y, 1.0f, false));
-  out.w = __builtin_bit_cast(float, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.y, 1.0f, true));
+  out.x = __builtin_bit_cast(float, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.x, scale, false));
+  out.y = __builtin_bit_cast(float, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.x, scale, true));
+  out.z = __builtin_bit_cast(float, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.y, scale, false));
+  out.w = __builtin_bit_cast(float, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v.y, scale, true));
   return out;
 }
 
-template <int BN, int BK, bool X8>
+template <int BN, int BK, bool X8, bool A8>
 __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S, int64_t Npad, float* __restrict__ slab,
                                            int64_t slab_elems, char* smem) {
   constexpr int WN = BN / 64, WK0 = 8 / WN, WK = (BK / 16 < WK0) ? BK / 16 : WK0, KTW = BK / WK / 16;
   static_assert(KTW >= 1 && WN * WK <= 8, "dW wave tiling");
   constexpr int XEB = X8 ? 1 : 2, RBX = BK * XEB;             // X element bytes, X image row bytes
-  constexpr int AB = PM_SPTS * BN * 2, XB = PM_SPTS * RBX;    // image bytes
+  constexpr int AEB = A8 ? 1 : 2, RBA = BN * AEB;
+  static_assert(Cfg<bf16_t>::M == 4 * PM_SPTS, "an fp8 scale covers 4 dW stages");
+  constexpr int AB = PM_SPTS * RBA, XB = PM_SPTS * RBX;       // image bytes
   constexpr int NI = (AB + XB + 1023) / 1024, PW = (NI + 7) / 8;  // DMA wave-instructions per stage / per wave
   static_assert((AB + XB) % 1024 == 0, "pm dW images: whole DMA wave-instructions");
   static_assert(PW * 8 * 1024 <= DW_STAGE_BYTES, "pm dW stage");
@@ -1892,9 +2033,12 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
     const int ii = 8 * i + wave;
     const int b = (ii < NI ? ii : 0) * 1024 + lane * 16;
     if (b < AB) {
-      const int r = b / (2 * BN), c = ((b % (2 * BN)) / 16) ^ pm_swz<2 * BN>(r);
-      src[i] = (const char*)J.A + ((int64_t)r * J.a_ld + 8 * (c < J.a_chunks ? c : 0)) * 2;
-      adv[i] = (int64_t)PM_SPTS * J.a_ld * 2;
+      const int r = b / RBA;
+      int c;
+      if constexpr (A8) c = ((b % RBA) / 16) ^ pm_swz8<RBA>(r);
+      else c = ((b % RBA) / 16) ^ pm_swz<RBA>(r);
+      src[i] = (const char*)J.A + (int64_t)r * J.a_ld * AEB + 16 * (c < J.a_chunks ? c : 0);
+      adv[i] = (int64_t)PM_SPTS * J.a_ld * AEB;
     } else if (b < AB + XB) {
       const int bx = b - AB, r = bx / RBX;
       int c;
@@ -1923,6 +2067,12 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
       __builtin_amdgcn_global_load_lds(src[i] + st * adv[i],
                                        (__attribute__((address_space(3))) void*)(dst + (8 * i + wave) * 1024), 16, 0, 0);
   };
+  float* const scl = (float*)(smem + PM_STAGES * DW_STAGE_BYTES);
+  const int64_t t0 = st_lo >> 2;
+  if constexpr (A8) {  // visible to every wave after the first stage's barrier (lgkmcnt(0) before it)
+    const int ntl = st_lo < st_hi ? (int)(((st_hi - 1) >> 2) - t0 + 1) : 0;
+    for (int i = tid; i < ntl; i += DW_THREADS) scl[i] = J.a_scale[t0 + i];
+  }
   const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
   const bool do_bias = (k0 == 0) && wk == 0;
   const float one2 = __uint_as_float(0x3f803f80u);  // two bf16 1.0 halves
@@ -1950,8 +2100,14 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
     const char* buf = smem + (int)(st % PM_STAGES) * DW_STAGE_BYTES;
     if (mma_wave) {
       f4 a[4];
+      if constexpr (A8) {
+        const float sa = scl[(st >> 2) - t0];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) a[nt] = pm_frag<2 * BN>(buf, wn * 64 + 16 * nt, lane);
+        for (int nt = 0; nt < 4; ++nt) a[nt] = pm_frag8<RBA>(buf, wn * 64 + 16 * nt, lane, sa);
+      } else {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) a[nt] = pm_frag<RBA>(buf, wn * 64 + 16 * nt, lane);
+      }
       constexpr int QG = KTW < 4 ? KTW : 4;
 #pragma unroll
       for (int q0 = 0; q0 < KTW; q0 += QG) {
@@ -2137,7 +2293,9 @@ __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S,
 template <typename T>
 __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t Npad, int S, float* __restrict__ slab) {
   // x3: two buffers of three 384-row bf16 planes (144 KB); otherwise the LDS-DMA ring
-  __shared__ __attribute__((aligned(16))) char smem[is_x3<T> ? 2 * 3 * 384 * 64 : (Cfg<T>::PM ? PM_STAGES : DW_STAGES) * DW_STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[is_x3<T>      ? 2 * 3 * 384 * 64
+                                                    : Cfg<T>::PM ? PM_STAGES * DW_STAGE_BYTES + PM_SCALES * 4
+                                                                 : DW_STAGES * DW_STAGE_BYTES];
   // 1-D grid in job order (heaviest first); inside a job, split-major so the k-tiles sharing a dZ slab run together
   const int b = blockIdx.x;
   int ji = 0;
@@ -2152,19 +2310,25 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   if constexpr (Cfg<T>::PM) {
     // the tile's X format: fp8 if its columns come from an fp8 section (a k-tile never mixes formats: host check)
     const bool x8 = (k0 < J.x0p) ? J.x0_u8 : J.x1_u8;
+    // and its A format: the 128 / 256-row tiles are gradient sections (fp8 under YANERF_BF16_G8), a 64-row tile is a
+    // narrow gradient section or the bf16 dU rows (host check in launch_bwd)
+    constexpr bool G8 = YANERF_BF16_G8;
     auto run = [&](auto xc) {
       constexpr bool X8 = decltype(xc)::value;
       if (J.bn == 256) {
-        if (bk == 256) dw_tile_pm<256, 256, X8>(J, k0, s, S, Npad, slab, se, smem);
-        else if (bk == 128) dw_tile_pm<256, 128, X8>(J, k0, s, S, Npad, slab, se, smem);
-        else dw_tile_pm<256, 64, X8>(J, k0, s, S, Npad, slab, se, smem);
+        if (bk == 256) dw_tile_pm<256, 256, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        else if (bk == 128) dw_tile_pm<256, 128, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        else dw_tile_pm<256, 64, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
       } else if (J.bn == 128) {
-        if (bk == 256) dw_tile_pm<128, 256, X8>(J, k0, s, S, Npad, slab, se, smem);
-        else if (bk == 128) dw_tile_pm<128, 128, X8>(J, k0, s, S, Npad, slab, se, smem);
-        else dw_tile_pm<128, 64, X8>(J, k0, s, S, Npad, slab, se, smem);
+        if (bk == 256) dw_tile_pm<128, 256, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        else if (bk == 128) dw_tile_pm<128, 128, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        else dw_tile_pm<128, 64, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+      } else if (G8 && J.a_u8) {
+        if (bk == 256) dw_tile_pm<64, 256, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        else dw_tile_pm<64, 128, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
       } else {
-        if (bk == 256) dw_tile_pm<64, 256, X8>(J, k0, s, S, Npad, slab, se, smem);
-        else dw_tile_pm<64, 128, X8>(J, k0, s, S, Npad, slab, se, smem);
+        if (bk == 256) dw_tile_pm<64, 256, X8, false>(J, k0, s, S, Npad, slab, se, smem);
+        else dw_tile_pm<64, 128, X8, false>(J, k0, s, S, Npad, slab, se, smem);
       }
     };
     if (x8) run(std::integral_constant<bool, true>{});
@@ -2256,10 +2420,15 @@ static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, const f
 #ifndef YANERF_DW_SMAX
 #define YANERF_DW_SMAX 64
 #endif
-static int dw_splits(int total_tiles, int64_t n_stages) {
+// (point-major: also enough splits that one split's fp8 gradient scales fit the tile's PM_SCALES LDS slots)
+static int dw_splits(int total_tiles, int64_t n_stages, bool pm) {
   int64_t S = (YANERF_DW_SMAX * 64 + total_tiles - 1) / total_tiles;
   if (S > n_stages) S = n_stages;
   if (S > YANERF_DW_SMAX) S = YANERF_DW_SMAX;
+  if (pm) {
+    const int64_t cap = 4LL * (PM_SCALES - 2);  // stages per split whose scale tiles fit
+    if (S < (n_stages + cap - 1) / cap) S = (n_stages + cap - 1) / cap;
+  }
   if (S < 1) S = 1;
   return (int)S;
 }
@@ -2335,6 +2504,13 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     return (const void*)((const char*)saved + off);
   };
   auto grow = [&](int64_t r) { return (const void*)((const char*)gradbuf + r * ld * es); };
+  int a_es = (int)es;  // point-major gradient section bytes per element (pm_grad)
+  auto gsec = [&](int64_t r, const float** scale) -> const void* {
+    int64_t so = -1;
+    const int64_t off = pm_grad_sec(L.L, Npad, r, &a_es, &so);
+    *scale = so < 0 ? nullptr : (const float*)((const char*)gradbuf + so);
+    return (const void*)((const char*)gradbuf + off);
+  };
   D.n = 0;
   D.total_tiles = 0;
   D.slab_elems = 0;
@@ -2342,7 +2518,12 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     DwJob& j = D.j[D.n++];
     j.A = grow(sp.arow); j.a_rows = sp.a_rows;
     j.x0_u8 = j.x1_u8 = 0;
+    j.a_u8 = 0;
+    j.a_scale = nullptr;
+    a_es = (int)es;
     if (pm) {
+      j.A = gsec(sp.arow, &j.a_scale);
+      j.a_u8 = a_es == 1;
       j.X0 = psec(sp.x0, &j.x0_u8);
       j.X1 = psec(sp.x1, &j.x1_u8);
     } else {
@@ -2352,8 +2533,8 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     j.x0_rows = sp.x0_rows; j.x1_rows = sp.x1_rows;
     j.ktot = sp.x0_rows + sp.x1_rows;
     j.a_ld = sp.a_w; j.x0_ld = sp.x0_w; j.x1_ld = sp.x1_w;
-    if (pm) j.A = (const char*)j.A + (int64_t)sp.a_col * es;
-    j.a_chunks = (sp.a_w - sp.a_col) / 8;
+    if (pm) j.A = (const char*)j.A + (int64_t)sp.a_col * a_es;
+    j.a_chunks = (sp.a_w - sp.a_col) * a_es / 16;
     j.x0p = dw_x0p(L, pm, sp);
     j.ktot_v = j.x0p + sp.x1_rows;
     j.bn = dw_bn(sp.a_rows);
@@ -2413,9 +2594,8 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   const int64_t Npad = npad_of(prec, N);
   const typename Cfg<T>::w_t* Wt = (const typename Cfg<T>::w_t*)packed;
   const float* Wf = (const float*)((const char*)packed + L.f_base);
-  const GradRows GR = grad_rows(L.L, Cfg<T>::PM);
   ST* gradbuf = (ST*)ws;
-  int64_t grad_bytes = GR.rows * (Cfg<T>::PM ? Npad : row_ld(Npad, sizeof(ST))) * (int64_t)sizeof(ST);
+  const int64_t grad_bytes = grad_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM);
   float* slab = (float*)((char*)ws + grad_bytes);
   const uint64_t* masks = (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM));
   if (phase & 1) {
@@ -2431,7 +2611,10 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   for (int i = 0; i < D.n; ++i)  // a point-major k-tile reads one X format: mixed sections must split at a tile edge
     YN_CHECK(!D.j[i].X1 || D.j[i].x0_u8 == D.j[i].x1_u8 || D.j[i].x0p % dw_bkmax(prec) == 0,
              "mlp_backward: dW job %d mixes fp8 and bf16 columns inside a tile", i);
-  const int S = dw_splits(D.total_tiles, Npad / dw_stage_pts(prec));
+  for (int i = 0; i < D.n; ++i)  // the dW tile's A format follows its row tile (dw_tile_pm's A8)
+    YN_CHECK(!Cfg<T>::PM || D.j[i].bn == 64 || D.j[i].a_u8 == YANERF_BF16_G8,
+             "mlp_backward: dW job %d: gradient format %d does not match its %d-row tile", i, D.j[i].a_u8, D.j[i].bn);
+  const int S = dw_splits(D.total_tiles, Npad / dw_stage_pts(prec), Cfg<T>::PM);
   if (dw) {
     hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)(D.total_tiles * S)), dim3(DW_THREADS), 0, st, D, Npad, S,
                        slab);
@@ -2493,12 +2676,10 @@ int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, 
   if (check_desc(d)) return -1;
   MlpLayout L = make_layout(d, precision);
   const int64_t Npad = npad_of(precision, n_points);
-  const bool pm = prec_pm(precision);
-  const GradRows GR = grad_rows(d->n_layers, pm);
-  int64_t grad_bytes = GR.rows * (pm ? Npad : row_ld(Npad, elem_size(precision))) * (int64_t)elem_size(precision);
+  const int64_t grad_bytes = grad_t_bytes(d->n_layers, Npad, elem_size(precision), prec_pm(precision));
   int tiles = 0;
   int64_t se = dw_slab_elems_for(L, precision, &tiles);
-  int S = dw_splits(tiles, Npad / dw_stage_pts(precision));
+  int S = dw_splits(tiles, Npad / dw_stage_pts(precision), prec_pm(precision));
   return grad_bytes + (int64_t)S * se * 4;
 }
 

@@ -69,6 +69,9 @@ template <typename T> struct Cfg;
 #ifndef YANERF_BF16_PM
 #define YANERF_BF16_PM 1
 #endif
+#ifndef YANERF_PM_SPTS
+#define YANERF_PM_SPTS 64  // points per point-major dW stage (PM_SPTS below)
+#endif
 // PM: saved activations / backward gradients stored point-major in per-section arrays ([Npad][width], written from the
 // LDS tile with 16-byte stores, read by the dW kernel with transposed LDS reads) instead of feature-major rows
 #ifndef YANERF_F32_M
@@ -1730,6 +1733,7 @@ constexpr int DW_STAGES = YANERF_DW_STAGES, DW_STAGE_BYTES = 512 * DW_RB;
 constexpr int X3_SPTS = 32;
 static int64_t dw_stage_pts(int prec) {
   if (prec == YANERF_PREC_F32X3) return X3_SPTS;
+  if (prec == YANERF_PREC_BF16 && YANERF_BF16_PM) return YANERF_PM_SPTS;
   return (prec == YANERF_PREC_F32 ? Cfg<float>::KB : Cfg<bf16_t>::KB) * (DW_CPR / 4);
 }
 __device__ __forceinline__ int dw_swz(int row, int c) {
@@ -1952,14 +1956,16 @@ __device__ __forceinline__ int pm_swz(int r) {
   if constexpr (ROWB == 128) return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
   else return 2 * ((r & 3) | (((r >> 3) & 1) << 2));
 }
-constexpr int PM_SPTS = 32;  // points per dW stage
+constexpr int PM_SPTS = YANERF_PM_SPTS;  // points per dW stage: one or two 32-point K-blocks (images stacked)
+constexpr int PM_KBS = PM_SPTS / 32;
+static_assert(PM_SPTS == 32 || PM_SPTS == 64, "pm dW stage: 32 or 64 points");
 #ifndef YANERF_PM_STAGES
-#define YANERF_PM_STAGES 4
+#define YANERF_PM_STAGES (PM_KBS == 1 ? 4 : 3)
 #endif
 constexpr int PM_STAGES = YANERF_PM_STAGES;  // LDS-DMA ring depth of the point-major (bf16) dW tile
 // stage buffer: the widest image pair (A + X, 32 points) of any instantiation
 #ifndef YANERF_PM_STAGE_KB
-#define YANERF_PM_STAGE_KB (YANERF_BF16_G8 ? 24 : 32)
+#define YANERF_PM_STAGE_KB ((YANERF_BF16_G8 ? 24 : 32) * PM_KBS)
 #endif
 constexpr int PM_STAGE_BYTES = YANERF_PM_STAGE_KB * 1024;
 // wait until this wave's DMA of the stage about to be read has landed, given how many stages it issued after that
@@ -2029,7 +2035,8 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
   static_assert(KTW >= 1 && WN * WK <= 8, "dW wave tiling");
   constexpr int XEB = X8 ? 1 : 2, RBX = BK * XEB;             // X element bytes, X image row bytes
   constexpr int AEB = A8 ? 1 : 2, RBA = BN * AEB;
-  static_assert(Cfg<bf16_t>::M == 4 * PM_SPTS, "an fp8 scale covers 4 dW stages");
+  constexpr int SPT = Cfg<bf16_t>::M / PM_SPTS;  // stages per fp8 scale tile
+  static_assert(SPT * PM_SPTS == Cfg<bf16_t>::M, "an fp8 scale covers whole dW stages");
   constexpr int AB = PM_SPTS * RBA, XB = PM_SPTS * RBX;       // image bytes
   constexpr int NI = (AB + XB + 1023) / 1024, PW = (NI + 7) / 8;  // DMA wave-instructions per stage / per wave
   static_assert((AB + XB) % 1024 == 0, "pm dW images: whole DMA wave-instructions");
@@ -2085,9 +2092,9 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
                                        (__attribute__((address_space(3))) void*)(dst + (8 * i + wave) * 1024), 16, 0, 0);
   };
   float* const scl = (float*)(smem + PM_STAGES * PM_STAGE_BYTES);
-  const int64_t t0 = st_lo >> 2;
+  const int64_t t0 = st_lo / SPT;
   if constexpr (A8) {  // visible to every wave after the first stage's barrier (lgkmcnt(0) before it)
-    const int ntl = st_lo < st_hi ? (int)(((st_hi - 1) >> 2) - t0 + 1) : 0;
+    const int ntl = st_lo < st_hi ? (int)((st_hi - 1) / SPT - t0 + 1) : 0;
     for (int i = tid; i < ntl; i += DW_THREADS) scl[i] = J.a_scale[t0 + i];
   }
   const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
@@ -2112,15 +2119,20 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
     __builtin_amdgcn_s_barrier();
     if (st + PM_STAGES - 1 < st_hi) issue(st + PM_STAGES - 1);
     const char* buf = smem + ((int)st % PM_STAGES) * PM_STAGE_BYTES;
+#pragma unroll
+    for (int kb = 0; kb < PM_KBS; ++kb)
     if (mma_wave) {
+      // K-block kb of the stage: 32-point images at kb * 32 rows (the row swizzles repeat every 16 rows)
+      const char* bufa = buf + kb * 32 * RBA;
+      const char* bufx = buf + AB + kb * 32 * RBX;
       f4 a[4];
       if constexpr (A8) {
-        const float sa = scl[(st >> 2) - t0];
+        const float sa = scl[st / SPT - t0];
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) a[nt] = pm_frag8<RBA>(buf, wn * 64 + 16 * nt, lane, sa);
+        for (int nt = 0; nt < 4; ++nt) a[nt] = pm_frag8<RBA>(bufa, wn * 64 + 16 * nt, lane, sa);
       } else {
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) a[nt] = pm_frag<RBA>(buf, wn * 64 + 16 * nt, lane);
+        for (int nt = 0; nt < 4; ++nt) a[nt] = pm_frag<RBA>(bufa, wn * 64 + 16 * nt, lane);
       }
       constexpr int QG = KTW < 4 ? KTW : 4;
 #pragma unroll
@@ -2128,8 +2140,8 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
         f4 b[QG];
 #pragma unroll
         for (int q = 0; q < QG; ++q) {
-          if constexpr (X8) b[q] = pm_frag8<RBX>(buf + AB, (wk * KTW + q0 + q) * 16, lane);
-          else b[q] = pm_frag<RBX>(buf + AB, (wk * KTW + q0 + q) * 16, lane);
+          if constexpr (X8) b[q] = pm_frag8<RBX>(bufx, (wk * KTW + q0 + q) * 16, lane);
+          else b[q] = pm_frag<RBX>(bufx, (wk * KTW + q0 + q) * 16, lane);
         }
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
@@ -2442,7 +2454,7 @@ static int dw_splits(int total_tiles, int64_t n_stages, bool pm) {
   if (S > n_stages) S = n_stages;
   if (S > YANERF_DW_SMAX) S = YANERF_DW_SMAX;
   if (pm) {
-    const int64_t cap = 4LL * (PM_SCALES - 2);  // stages per split whose scale tiles fit
+    const int64_t cap = (int64_t)(Cfg<bf16_t>::M / PM_SPTS) * (PM_SCALES - 2);  // stages per split whose scales fit
     if (S < (n_stages + cap - 1) / cap) S = (n_stages + cap - 1) / cap;
   }
   if (S < 1) S = 1;

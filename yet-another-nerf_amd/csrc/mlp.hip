@@ -214,22 +214,29 @@ __host__ __device__ inline int64_t row_ld(int64_t Npad, size_t es) {
 #define YANERF_BF16_A8 1
 #endif
 constexpr int PM_HB = YANERF_BF16_A8 ? 1 : 2;  // bytes per saved H / C element
+// Y (intermediate_linear's output, signed, the X operand of color_layer.0's weight gradient only) as fp8 e4m3 with a
+// power-of-two scale per 128-point tile, like the backward's gradient rows (YANERF_BF16_G8)
+#ifndef YANERF_BF16_Y8
+#define YANERF_BF16_Y8 1
+#endif
+constexpr int PM_YB = YANERF_BF16_Y8 ? 1 : 2;
 struct PmSave {
-  int64_t pe, h0, y, dpe, c, total;
+  int64_t pe, h0, y, dpe, c, ysc, total;
 };
 __host__ __device__ inline PmSave pm_save(int L, int64_t Npad) {
   PmSave s;
   int64_t o = 0;
   s.pe = o; o += 2LL * KPE * Npad;
   s.h0 = o; o += (int64_t)PM_HB * 256 * L * Npad;
-  s.y = o; o += 2LL * 256 * Npad;
+  s.y = o; o += (int64_t)PM_YB * 256 * Npad;
   s.dpe = o; o += 2LL * KDIR * Npad;
   s.c = o; o += (int64_t)PM_HB * HC * Npad;
-  s.total = o;
+  s.ysc = o; o += 4LL * (Npad / 128);
+  s.total = (o + 255) / 256 * 256;
   return s;
 }
 // byte offset and element bytes of the saved section that starts at SavedRows row r0 (point-major bf16 layout)
-static int64_t pm_sec_bytes(int L, int64_t Npad, int64_t r0, int* es) {
+static int64_t pm_sec_bytes(int L, int64_t Npad, int64_t r0, int* es, int64_t* scale_off = nullptr) {
   const SavedRows SR = saved_rows(L);
   const PmSave PS = pm_save(L, Npad);
   *es = 2;
@@ -238,7 +245,11 @@ static int64_t pm_sec_bytes(int L, int64_t Npad, int64_t r0, int* es) {
     *es = PM_HB;
     return PS.h0 + (r0 - SR.h0) / 256 * (int64_t)PM_HB * 256 * Npad;
   }
-  if (r0 == SR.y) return PS.y;
+  if (r0 == SR.y) {
+    *es = PM_YB;
+    if (scale_off && YANERF_BF16_Y8) *scale_off = PS.ysc;
+    return PS.y;
+  }
   if (r0 == SR.dpe) return PS.dpe;
   *es = PM_HB;
   return PS.c;  // r0 == SR.c
@@ -1194,10 +1205,10 @@ __device__ __forceinline__ float g8_scale(float amax) {
   return e <= 7u ? 1.0f : __uint_as_float((e - 7u) << 23);
 }
 // the gradient tile's save: `red` holds each wave's |max| of the section (written before the last barrier)
-template <typename T, int NTHR, int W>
+template <typename T, int NTHR, int W, bool F8 = YANERF_BF16_G8>
 __device__ __forceinline__ void save_grad_pm(const typename Cfg<T>::lds_t* act, char* dst, float* scale_out,
                                              const float* red, int waves, int tid) {
-  if constexpr (YANERF_BF16_G8) {
+  if constexpr (F8) {
     float amax = red[0];
     for (int w = 1; w < waves; ++w) amax = fmaxf(amax, red[w]);
     const float sc = g8_scale(amax);
@@ -1355,7 +1366,11 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     }
   }
   lds_barrier();
+  // fp8 Y: each wave's |max| of Y in the PE columns 32.. of row 16 (free once the trunk is done: the direction
+  // embedding takes columns 0..31), read by the Y save after the colour GEMM
+  [[maybe_unused]] float* const yred = (float*)(act + 16 * ROW + PE_COL + 32);
   {
+    G8Max gmax;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int n = nrow0 + 16 * nt + 4 * g;
@@ -1365,9 +1380,15 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
         const int m = 16 * mt + li;
         const Pk<T> h = pk_make<T>(v);
         pk_lds<T>(act, m, n, h);
+        if constexpr (PM && YANERF_BF16_Y8) gmax.add(h);
         if (sv && !PM) pk_store_rows_b<T>((saved + (SR.y + nrow0 + 16 * nt) * ld + p0),
                              soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
       }
+    }
+    if constexpr (PM && YANERF_BF16_Y8) {
+      static_assert(PE_COL + 32 + 2 * WAVES <= ROW, "Y scale slots");
+      const float am = wave_max(gmax.value());
+      if (sv && lane == 0) yred[wave] = am;
     }
   }
   // ---- direction embedding of normalize(d) (nerf_mlp.py:105-108) into cols 256..287
@@ -1385,7 +1406,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     gemm_lds<T, NTC, MT>(Wt + lay.wc_off, wpl, KC, crow0, act, 0, KC / KB, accc, lane, Wf + lay.bc_off, &ringc);
     if constexpr (PM) {
       if (sv) {
-        copy_tile_pm<T, NTHR, 256>(act, 0, (ST*)((char*)saved + PS.y) + p0 * 256, tid);
+        save_grad_pm<T, NTHR, 256, YANERF_BF16_Y8>(act, (char*)saved + PS.y + p0 * 256 * PM_YB,
+                                                   (float*)((char*)saved + PS.ysc) + blockIdx.x, yred, WAVES, tid);
         copy_tile_pm<T, NTHR, KDIR>(act, PE_COL, (ST*)((char*)saved + PS.dpe) + p0 * KDIR, tid);
       }
     }
@@ -1679,6 +1701,7 @@ struct DwJob {
   int x0_u8, x1_u8;  // X0 / X1 stored as fp8 e4m3 (YANERF_BF16_A8: the post-ReLU sections); a k-tile is one format
   int a_u8;          // A stored as fp8 e4m3 of value / scale (YANERF_BF16_G8: dZ_l, dY, dZc; not dU)
   const float* a_scale;  // A's decode scale per 128-point tile
+  const float* x_scale;  // X0's decode scale per 128-point tile (fp8 Y), or null
 };
 constexpr int kMaxDwJobs = MAXL + 4;
 struct DwJobs {
@@ -1959,15 +1982,16 @@ __device__ __forceinline__ int pm_swz(int r) {
 constexpr int PM_SPTS = YANERF_PM_SPTS;  // points per dW stage: one or two 32-point K-blocks (images stacked)
 constexpr int PM_KBS = PM_SPTS / 32;
 static_assert(PM_SPTS == 32 || PM_SPTS == 64, "pm dW stage: 32 or 64 points");
-#ifndef YANERF_PM_STAGES
-#define YANERF_PM_STAGES (PM_KBS == 1 ? 4 : 3)
-#endif
-constexpr int PM_STAGES = YANERF_PM_STAGES;  // LDS-DMA ring depth of the point-major (bf16) dW tile
 // stage buffer: the widest image pair (A + X, 32 points) of any instantiation
 #ifndef YANERF_PM_STAGE_KB
-#define YANERF_PM_STAGE_KB ((YANERF_BF16_G8 ? 24 : 32) * PM_KBS)
+#define YANERF_PM_STAGE_KB ((YANERF_BF16_G8 ? (YANERF_BF16_Y8 ? 16 : 24) : 32) * PM_KBS)
 #endif
 constexpr int PM_STAGE_BYTES = YANERF_PM_STAGE_KB * 1024;
+// LDS-DMA ring depth of the point-major (bf16) dW tile: as many stages as fit 128 KB
+#ifndef YANERF_PM_STAGES
+#define YANERF_PM_STAGES (128 / YANERF_PM_STAGE_KB)
+#endif
+constexpr int PM_STAGES = YANERF_PM_STAGES;
 // wait until this wave's DMA of the stage about to be read has landed, given how many stages it issued after that
 // one: vmcnt(PW * min(ahead, MAXA)) (the count must be an immediate)
 template <int PW, int MAXA>
@@ -2093,9 +2117,15 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
   };
   float* const scl = (float*)(smem + PM_STAGES * PM_STAGE_BYTES);
   const int64_t t0 = st_lo / SPT;
-  if constexpr (A8) {  // visible to every wave after the first stage's barrier (lgkmcnt(0) before it)
+  // X0's scales (fp8 Y) in the next PM_SCALES slots, for the k-tiles over X0
+  const bool xs = X8 && J.x_scale && k0 < J.x0p;
+  float* const sclx = scl + PM_SCALES;
+  {  // visible to every wave after the first stage's barrier (lgkmcnt(0) before it)
     const int ntl = st_lo < st_hi ? (int)((st_hi - 1) / SPT - t0 + 1) : 0;
-    for (int i = tid; i < ntl; i += DW_THREADS) scl[i] = J.a_scale[t0 + i];
+    if constexpr (A8)
+      for (int i = tid; i < ntl; i += DW_THREADS) scl[i] = J.a_scale[t0 + i];
+    if (xs)
+      for (int i = tid; i < ntl; i += DW_THREADS) sclx[i] = J.x_scale[t0 + i];
   }
   const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
   const bool do_bias = (k0 == 0) && wk == 0;
@@ -2126,6 +2156,7 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
       const char* bufa = buf + kb * 32 * RBA;
       const char* bufx = buf + AB + kb * 32 * RBX;
       f4 a[4];
+      const float sx = xs ? sclx[st / SPT - t0] : 1.0f;
       if constexpr (A8) {
         const float sa = scl[st / SPT - t0];
 #pragma unroll
@@ -2140,7 +2171,7 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
         f4 b[QG];
 #pragma unroll
         for (int q = 0; q < QG; ++q) {
-          if constexpr (X8) b[q] = pm_frag8<RBX>(bufx, (wk * KTW + q0 + q) * 16, lane);
+          if constexpr (X8) b[q] = pm_frag8<RBX>(bufx, (wk * KTW + q0 + q) * 16, lane, sx);
           else b[q] = pm_frag<RBX>(bufx, (wk * KTW + q0 + q) * 16, lane);
         }
 #pragma unroll
@@ -2316,11 +2347,24 @@ __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S,
   }
 }
 
+// stage bytes of a point-major dW tile; the dispatch below only instantiates the tiles that fit PM_STAGE_BYTES (the
+// host checks every job's tiles against the same function before the launch)
+__host__ __device__ constexpr int pm_tile_bytes(int bn, int bk, bool x8, bool a8) {
+  return PM_SPTS * (bn * (a8 ? 1 : 2) + bk * (x8 ? 1 : 2));
+}
+template <int BN, int BK, bool X8, bool A8>
+__device__ __forceinline__ void run_pm(const DwJob& J, int k0, int s, int S, int64_t Npad, float* __restrict__ slab,
+                                       int64_t slab_elems, char* smem) {
+  if constexpr (pm_tile_bytes(BN, BK, X8, A8) <= PM_STAGE_BYTES)
+    dw_tile_pm<BN, BK, X8, A8>(J, k0, s, S, Npad, slab, slab_elems, smem);
+  // else: not instantiated; launch_bwd refuses a job with such a tile before the launch
+}
+
 template <typename T>
 __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t Npad, int S, float* __restrict__ slab) {
   // x3: two buffers of three 384-row bf16 planes (144 KB); otherwise the LDS-DMA ring
   __shared__ __attribute__((aligned(16))) char smem[is_x3<T>      ? 2 * 3 * 384 * 64
-                                                    : Cfg<T>::PM ? PM_STAGES * PM_STAGE_BYTES + PM_SCALES * 4
+                                                    : Cfg<T>::PM ? PM_STAGES * PM_STAGE_BYTES + 2 * PM_SCALES * 4
                                                                  : DW_STAGES * DW_STAGE_BYTES];
   // 1-D grid in job order (heaviest first); inside a job, split-major so the k-tiles sharing a dZ slab run together.
   // (An XCD-aware order -- the tiles of jobs that share a section as consecutive blocks of one XCD -- measured slower:
@@ -2344,19 +2388,19 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
     auto run = [&](auto xc) {
       constexpr bool X8 = decltype(xc)::value;
       if (J.bn == 256) {
-        if (bk == 256) dw_tile_pm<256, 256, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
-        else if (bk == 128) dw_tile_pm<256, 128, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
-        else dw_tile_pm<256, 64, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        if (bk == 256) run_pm<256, 256, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        else if (bk == 128) run_pm<256, 128, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        else run_pm<256, 64, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
       } else if (J.bn == 128) {
-        if (bk == 256) dw_tile_pm<128, 256, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
-        else if (bk == 128) dw_tile_pm<128, 128, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
-        else dw_tile_pm<128, 64, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        if (bk == 256) run_pm<128, 256, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        else if (bk == 128) run_pm<128, 128, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        else run_pm<128, 64, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
       } else if (G8 && J.a_u8) {
-        if (bk == 256) dw_tile_pm<64, 256, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
-        else dw_tile_pm<64, 128, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        if (bk == 256) run_pm<64, 256, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        else run_pm<64, 128, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
       } else {
-        if (bk == 256) dw_tile_pm<64, 256, X8, false>(J, k0, s, S, Npad, slab, se, smem);
-        else dw_tile_pm<64, 128, X8, false>(J, k0, s, S, Npad, slab, se, smem);
+        if (bk == 256) run_pm<64, 256, X8, false>(J, k0, s, S, Npad, slab, se, smem);
+        else run_pm<64, 128, X8, false>(J, k0, s, S, Npad, slab, se, smem);
       }
     };
     if (x8) run(std::integral_constant<bool, true>{});
@@ -2508,11 +2552,13 @@ static void for_each_dw_job(const MlpLayout& L, bool pm, F&& f) {
 }
 
 // X0's padded width in a point-major tile: whole 16-byte chunks (8 bf16 / 16 fp8 columns)
+// (a whole number of k-tiles when X1 has the other element format: a k-tile reads one format)
 static int dw_x0p(const MlpLayout& L, bool pm, const DwSpec& sp) {
   if (!pm) return sp.x0_rows;
-  int es = 2;
+  int es = 2, es1 = 2;
   pm_sec_bytes(L.L, 128, sp.x0, &es);
-  const int q = es == 1 ? 16 : 8;
+  if (sp.x1 >= 0) pm_sec_bytes(L.L, 128, sp.x1, &es1);
+  const int q = (sp.x1 >= 0 && es1 != es) ? dw_bkmax(YANERF_PREC_BF16) : (es == 1 ? 16 : 8);
   return (sp.x0_rows + q - 1) / q * q;
 }
 
@@ -2523,12 +2569,15 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
   const int64_t ld = pm ? Npad : row_ld(Npad, es);
   auto srow = [&](int64_t r) { return r < 0 ? nullptr : (const void*)((const char*)saved + r * ld * es); };
   // point-major (bf16): sections at byte offsets, some in fp8 (pm_save)
-  auto psec = [&](int64_t r, int* u8) -> const void* {
+  auto psec = [&](int64_t r, int* u8, const float** scale) -> const void* {
     *u8 = 0;
+    *scale = nullptr;
     if (r < 0) return nullptr;
     int b = 2;
-    const int64_t off = pm_sec_bytes(L.L, Npad, r, &b);
+    int64_t so = -1;
+    const int64_t off = pm_sec_bytes(L.L, Npad, r, &b, &so);
     *u8 = b == 1;
+    if (so >= 0) *scale = (const float*)((const char*)saved + so);
     return (const void*)((const char*)saved + off);
   };
   auto grow = [&](int64_t r) { return (const void*)((const char*)gradbuf + r * ld * es); };
@@ -2548,12 +2597,14 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     j.x0_u8 = j.x1_u8 = 0;
     j.a_u8 = 0;
     j.a_scale = nullptr;
+    j.x_scale = nullptr;
     a_es = (int)es;
     if (pm) {
       j.A = gsec(sp.arow, &j.a_scale);
       j.a_u8 = a_es == 1;
-      j.X0 = psec(sp.x0, &j.x0_u8);
-      j.X1 = psec(sp.x1, &j.x1_u8);
+      const float* x1s = nullptr;  // (never scaled: the second inputs are the PE sections)
+      j.X0 = psec(sp.x0, &j.x0_u8, &j.x_scale);
+      j.X1 = psec(sp.x1, &j.x1_u8, &x1s);
     } else {
       j.X0 = srow(sp.x0);
       j.X1 = srow(sp.x1);
@@ -2639,6 +2690,16 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   for (int i = 0; i < D.n; ++i)  // a point-major k-tile reads one X format: mixed sections must split at a tile edge
     YN_CHECK(!D.j[i].X1 || D.j[i].x0_u8 == D.j[i].x1_u8 || D.j[i].x0p % dw_bkmax(prec) == 0,
              "mlp_backward: dW job %d mixes fp8 and bf16 columns inside a tile", i);
+  if (Cfg<T>::PM)  // every k-tile's images fit the stage buffer (run_pm)
+    for (int i = 0; i < D.n; ++i)
+      for (int kt = 0; kt < D.j[i].k_tiles; ++kt) {
+        const DwJob& j = D.j[i];
+        const int k0 = kt * dw_bkmax(prec), bk = kt < j.k_full ? dw_bkmax(prec) : j.bk_tail;
+        const bool x8 = (k0 < j.x0p) ? j.x0_u8 : j.x1_u8;
+        YN_CHECK(pm_tile_bytes(j.bn, bk, x8, j.a_u8) <= PM_STAGE_BYTES,
+                 "mlp_backward: dW job %d k-tile %d needs %d B per stage (> %d)", i, kt,
+                 pm_tile_bytes(j.bn, bk, x8, j.a_u8), PM_STAGE_BYTES);
+      }
   for (int i = 0; i < D.n; ++i)  // the dW tile's A format follows its row tile (dw_tile_pm's A8)
     YN_CHECK(!Cfg<T>::PM || D.j[i].bn == 64 || D.j[i].a_u8 == YANERF_BF16_G8,
              "mlp_backward: dW job %d: gradient format %d does not match its %d-row tile", i, D.j[i].a_u8, D.j[i].bn);

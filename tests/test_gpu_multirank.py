@@ -13,6 +13,8 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
+from mp_util import _as_tensors, _by_value
+
 pytestmark = pytest.mark.gpu
 
 H, W, N_VIEWS = 13, 20, 5  # odd row count and a view count that is not a multiple of the world size
@@ -60,7 +62,7 @@ def _worker(rank, world, port, q):
     f, c, d = tr.render(pose, focal, H, W, chunk=97, shard=True)
     ev = tr.evaluate(views)
     torch.cuda.synchronize()
-    q.put((rank, f.cpu(), c.cpu(), d.cpu(), ev))
+    q.put(_by_value((rank, f.cpu(), c.cpu(), d.cpu(), ev)))
     parallel.barrier()
     torch.distributed.destroy_process_group()
 
@@ -82,7 +84,7 @@ def test_sharded_render_and_evaluate_two_ranks():
         deadline = time.monotonic() + 150
         while len(res) < world and time.monotonic() < deadline:
             try:
-                res.append(q.get(timeout=2))
+                res.append(_as_tensors(q.get(timeout=2)))
             except queue.Empty:
                 assert all(p.is_alive() or p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
         res.sort(key=lambda x: x[0])
@@ -113,7 +115,7 @@ def _spawn(target, world, extra=()):
         deadline = time.monotonic() + 150
         while len(res) < world and time.monotonic() < deadline:
             try:
-                res.append(q.get(timeout=2))
+                res.append(_as_tensors(q.get(timeout=2)))
             except queue.Empty:
                 assert all(p.is_alive() or p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
         res.sort(key=lambda x: x[0])
@@ -169,7 +171,7 @@ def _trainer_worker(rank, world, port, q):
         out.append(dict(local=local[-1], reduced=tr.flat.grad.detach().cpu().clone(),
                         params=tr.flat.data.detach().cpu().clone(), xys=tr.xys.detach().cpu().clone(), lr=tr.lr))
     parallel.allreduce_mean_ = orig
-    q.put((rank, out))
+    q.put(_by_value((rank, out)))
     parallel.barrier()
     torch.distributed.destroy_process_group()
 
@@ -232,7 +234,7 @@ def _ddp_worker(rank, world, port, q, golden_dir):
 
     reduced = run(ddp)
     local = run(pipe)
-    q.put((rank, local, reduced))
+    q.put(_by_value((rank, local, reduced)))
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
 

@@ -6,6 +6,7 @@ import socket
 
 import torch
 import torch.multiprocessing as mp
+from mp_util import _as_tensors, _by_value
 
 import yanerf_boot  # noqa: F401
 
@@ -33,7 +34,7 @@ def _worker(rank, world, port, q):
     m = parallel.allgather_cat(torch.tensor([float(rank)]))
     mx = parallel.max_over_ranks(float(rank) + 0.5)
     shards = [list(parallel.shard_range(10, k, world)) for k in range(world)]
-    q.put((rank, fp.data.clone(), lin[0].grad.clone(), m, mx, shards))
+    q.put(_by_value((rank, fp.data.clone(), lin[0].grad.clone(), m, mx, shards)))
     parallel.barrier()
     torch.distributed.destroy_process_group()
 
@@ -45,7 +46,7 @@ def test_gloo_world2():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    res = sorted([_as_tensors(q.get(timeout=120)) for _ in range(world)], key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -72,7 +73,7 @@ def _eval_worker(rank, world, port, q):
     img = torch.arange(H * W * 3, dtype=torch.float32).view(H, W, 3)
     rows = parallel.shard_range(H, rank, world)
     full = parallel.gather_rows(img[rows.start:rows.stop].clone(), H)
-    q.put((rank, gathered, full, parallel.world_rank()))
+    q.put(_by_value((rank, gathered, full, parallel.world_rank())))
     parallel.barrier()
     torch.distributed.destroy_process_group()
 
@@ -84,7 +85,7 @@ def test_gloo_world3_sharded_eval():
     procs = [ctx.Process(target=_eval_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    res = sorted([_as_tensors(q.get(timeout=120)) for _ in range(world)], key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

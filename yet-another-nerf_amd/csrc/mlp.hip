@@ -1713,6 +1713,7 @@ struct DwJobs {
   int n;
   int total_tiles;
   int64_t slab_elems;
+  int64_t slab_stride;  // elements between two splits' slabs: slab_elems padded to a multiple of 4 (dw_slab_pad)
 };
 constexpr int DW_THREADS = 512;
 // widest dW column tile: bf16 is HBM/L2-bound (a 256-wide tile reads each dZ row once), fp32 is MFMA-bound and
@@ -2056,11 +2057,54 @@ __device__ __forceinline__ f4 pm_frag8(const char* img, int f0, int lane, float 
   return out;
 }
 
+// fp8 x fp8 tiles on the block-scaled fp8 MFMA (YANERF_DW_F8MMA): a 64-point stage is ONE
+// v_mfma_scale_f32_32x32x64_f8f6f4 per 32 x 32 output tile (e4m3 operands, 64 cycles: twice the bf16 rate, and no
+// widening), with the stage's power-of-two tile scales as the operands' e8m0 scales (exact, like the widening they
+// replace). Operand map (tools/probes/probe_mfma_f8.hip, exact on the MI355X): lane l holds A[row l % 32][k = 32 (l / 32)
+// + j] and B[k = 32 (l / 32) + j][col l % 32] in byte j of its 8 dwords. With points as k, lane (g, i) of a 16-lane group
+// needs points 32 (g >> 1) + 0..31 of feature 16 (g & 1) + i: four ds_read_b64_tr_b8 (8 points each).
+#ifndef YANERF_DW_F8MMA
+#define YANERF_DW_F8MMA 1
+#endif
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+// image swizzle for those reads: a 32-lane half touches 8 consecutive rows x the chunk pair (c0, c0 ^ 1), c0 even, so
+// s(r) >> 1 must differ over the 8 rows (RB = 256) or over the 4 rows of one parity (RB = 128, two rows per bank sweep)
+template <int RB>
+__device__ __forceinline__ int f8m_swz(int r) {
+  static_assert(RB == 128 || RB == 256, "fp8 MFMA image row width");
+  if constexpr (RB == 256) return 2 * (r & 7);
+  else return 2 * ((r >> 1) & 3);
+}
+template <int RB>
+__device__ __forceinline__ i32x8 f8m_frag(const char* img, int f0, int lane) {
+  typedef int i32x2 __attribute__((ext_vector_type(2)));
+  const int g = lane >> 4, i = lane & 15, q = i >> 1, p = i & 1;
+  const int c = f0 / 16 + (g & 1);
+  i32x8 out;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int r = 32 * (g >> 1) + 8 * t + q;
+    const char* a = img + r * RB + 16 * (c ^ f8m_swz<RB>(r)) + 8 * p;
+    const i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) i32x2*)(a));
+    out[2 * t] = v.x;
+    out[2 * t + 1] = v.y;
+  }
+  return out;
+}
+// e8m0 exponent of a power-of-two float scale
+__device__ __forceinline__ int e8m0_of(float s) { return (int)((__float_as_uint(s) >> 23) & 0xffu); }
+template <int BN, int BK, bool X8, bool A8>
+constexpr bool use_f8mma() {
+  return YANERF_DW_F8MMA && X8 && A8 && BK == 256 && (BN == 256 || BN == 128) && YANERF_PM_SPTS == 64;
+}
+
 template <int BN, int BK, bool X8, bool A8>
 __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S, int64_t Npad, float* __restrict__ slab,
                                            int64_t slab_elems, char* smem) {
   constexpr int WN = BN / 64, WK0 = 8 / WN, WK = (BK / 16 < WK0) ? BK / 16 : WK0, KTW = BK / WK / 16;
   static_assert(KTW >= 1 && WN * WK <= 8, "dW wave tiling");
+  constexpr bool F8M = use_f8mma<BN, BK, X8, A8>();
   constexpr int XEB = X8 ? 1 : 2, RBX = BK * XEB;             // X element bytes, X image row bytes
   constexpr int AEB = A8 ? 1 : 2, RBA = BN * AEB;
   constexpr int SPT = Cfg<bf16_t>::M / PM_SPTS;  // stages per fp8 scale tile
@@ -2087,14 +2131,16 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
     if (b < AB) {
       const int r = b / RBA;
       int c;
-      if constexpr (A8) c = ((b % RBA) / 16) ^ pm_swz8<RBA>(r);
+      if constexpr (F8M) c = ((b % RBA) / 16) ^ f8m_swz<RBA>(r);
+      else if constexpr (A8) c = ((b % RBA) / 16) ^ pm_swz8<RBA>(r);
       else c = ((b % RBA) / 16) ^ pm_swz<RBA>(r);
       src[i] = (const char*)J.A + (int64_t)r * J.a_ld * AEB + 16 * (c < J.a_chunks ? c : 0);
       adv[i] = (int64_t)PM_SPTS * J.a_ld * AEB;
     } else if (b < AB + XB) {
       const int bx = b - AB, r = bx / RBX;
       int c;
-      if constexpr (X8) c = ((bx % RBX) / 16) ^ pm_swz8<RBX>(r);
+      if constexpr (F8M) c = ((bx % RBX) / 16) ^ f8m_swz<RBX>(r);
+      else if constexpr (X8) c = ((bx % RBX) / 16) ^ pm_swz8<RBX>(r);
       else c = ((bx % RBX) / 16) ^ pm_swz<RBX>(r);
       const int j = k0 + (16 / XEB) * c;  // virtual column
       if (j < J.x0p) {
@@ -2131,6 +2177,77 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
     if (xs)
       for (int i = tid; i < ntl; i += DW_THREADS) sclx[i] = J.x_scale[t0 + i];
   }
+  if constexpr (F8M) {
+    // wave tile: 64 rows (two 32-row MFMA tiles) x BK / WK columns (NQ 32-column tiles)
+    constexpr int WKF = 8 / WN, NQ = BK / WKF / 32;
+    static_assert(NQ >= 1 && WN * WKF == 8, "fp8 MFMA dW wave tiling");
+    const int wnf = wave / WKF, wkf = wave % WKF;
+    const bool do_bias = (k0 == 0) && wkf == 0;
+    const i32x8 ones = i32x8{0x38383838, 0x38383838, 0x38383838, 0x38383838,
+                             0x38383838, 0x38383838, 0x38383838, 0x38383838};  // e4m3 1.0
+    f16v acc[2][NQ], accb[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) accb[mt][e] = 0.f;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[mt][q][e] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < PM_STAGES - 1; ++i)
+      if (st_lo + i < st_hi) issue(st_lo + i);
+    for (int64_t st = st_lo; st < st_hi; ++st) {
+      const int64_t ahead = st_hi - 1 - st;
+      wait_dma_ahead<PW, PM_STAGES - 2>(ahead);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (st + PM_STAGES - 1 < st_hi) issue(st + PM_STAGES - 1);
+      const char* buf = smem + ((int)st % PM_STAGES) * PM_STAGE_BYTES;
+      const int sa = e8m0_of(scl[st / SPT - t0]);
+      const int sx = xs ? e8m0_of(sclx[st / SPT - t0]) : 127;
+      i32x8 a[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) a[mt] = f8m_frag<RBA>(buf, wnf * 64 + 32 * mt, lane);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const i32x8 b = f8m_frag<RBX>(buf + AB, (wkf * NQ + q) * 32, lane);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          acc[mt][q] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[mt], b, acc[mt][q], 0, 0, 0, sa, 0, sx);
+      }
+      if (do_bias) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          accb[mt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a[mt], ones, accb[mt], 0, 0, 0, sa, 0, 127);
+      }
+    }
+    // C/D: column lane & 31, row (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+    float* out = slab + (int64_t)s * slab_elems + J.slab_off;
+    const int kv = J.ktot + 1;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int j = k0 + (wkf * NQ + q) * 32 + (lane & 31);  // virtual column -> weight column
+      const int k = j < J.x0p ? (j < J.x0_rows ? j : -1) : (j - J.x0p < J.x1_rows ? J.x0_rows + j - J.x0p : -1);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int n = wnf * 64 + 32 * mt + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+          if (n < J.a_rows && k >= 0) out[(int64_t)n * kv + k] = acc[mt][q][e];
+        }
+    }
+    if (do_bias && (lane & 31) == 0) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int n = wnf * 64 + 32 * mt + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+          if (n < J.a_rows) out[(int64_t)n * kv + J.ktot] = accb[mt][e];
+        }
+    }
+  } else {
   const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
   const bool do_bias = (k0 == 0) && wk == 0;
   const float one2 = __uint_as_float(0x3f803f80u);  // two bf16 1.0 halves
@@ -2213,6 +2330,7 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
           if (n < J.a_rows) out[(int64_t)n * kv + J.ktot] = accb[nt][r];
         }
     }
+  }
   }
 }
 
@@ -2382,7 +2500,7 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   constexpr int BKMAX = dw_bkmax(prec_of<T>);
   const int k0 = kt * BKMAX;
   const int bk = kt < J.k_full ? BKMAX : J.bk_tail;
-  const int64_t se = jobs.slab_elems;
+  const int64_t se = jobs.slab_stride;
   if constexpr (Cfg<T>::PM) {
     // the tile's X format: fp8 if its columns come from an fp8 section (a k-tile never mixes formats: host check)
     const bool x8 = (k0 < J.x0p) ? J.x0_u8 : J.x1_u8;
@@ -2433,19 +2551,37 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   }
 }
 
+// Sums the S split slabs in split order (deterministic): a thread owns 4 consecutive slab elements and reads them as
+// one 16-byte load per split, 8 splits' loads in flight before their adds (the slab stride is padded to a multiple of
+// 4 elements, dw_slab_pad); the sum order per element is s = 0, 1, ..., S - 1 as before.
 __global__ void dw_reduce_kernel(DwJobs jobs, int S, const float* __restrict__ slab) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= jobs.slab_elems) return;
+  const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (e0 >= jobs.slab_elems) return;
+  const int64_t stride = jobs.slab_stride;
+  f4 sum = f4{0.f, 0.f, 0.f, 0.f};
+  int s = 0;
+  for (; s + 8 <= S; s += 8) {
+    f4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *(const f4*)(slab + (int64_t)(s + u) * stride + e0);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) sum += v[u];
+  }
+  for (; s < S; ++s) sum += *(const f4*)(slab + (int64_t)s * stride + e0);
+  const float vals[4] = {sum.x, sum.y, sum.z, sum.w};
   int ji = 0;
-  while (ji + 1 < jobs.n && jobs.j[ji + 1].slab_off <= e) ++ji;
-  const DwJob& J = jobs.j[ji];
-  const int64_t local = e - J.slab_off;
-  const int kv = J.ktot + 1;
-  const int n = (int)(local / kv), k = (int)(local % kv);
-  float sum = 0.0f;
-  for (int s = 0; s < S; ++s) sum += slab[(int64_t)s * jobs.slab_elems + e];
-  if (k < J.ktot) J.W[(int64_t)n * J.ktot + k] = sum;
-  else J.b[n] = sum;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t e = e0 + i;
+    if (e >= jobs.slab_elems) break;
+    while (ji + 1 < jobs.n && jobs.j[ji + 1].slab_off <= e) ++ji;
+    const DwJob& J = jobs.j[ji];
+    const int64_t local = e - J.slab_off;
+    const int kv = J.ktot + 1;
+    const int n = (int)(local / kv), k = (int)(local % kv);
+    if (k < J.ktot) J.W[(int64_t)n * J.ktot + k] = vals[i];
+    else J.b[n] = vals[i];
+  }
 }
 
 // ============================================================================================ host helpers
@@ -2493,14 +2629,20 @@ static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, const f
 }
 
 // point splits per dW tile: enough workgroups that the light jobs dispatched last fill the tail of the heavy ones
+// (fp32 / x3 64; bf16 32: its fp8-MFMA dW is bound by the operand stream, and half the splits halve the slab reduce,
+// measured dW 0.87 -> 0.84 ms and reduce 0.036 -> 0.020 ms at the Lego fine pass)
 #ifndef YANERF_DW_SMAX
 #define YANERF_DW_SMAX 64
 #endif
+#ifndef YANERF_DW_SMAX_PM
+#define YANERF_DW_SMAX_PM 32
+#endif
 // (point-major: also enough splits that one split's fp8 gradient scales fit the tile's PM_SCALES LDS slots)
 static int dw_splits(int total_tiles, int64_t n_stages, bool pm) {
-  int64_t S = (YANERF_DW_SMAX * 64 + total_tiles - 1) / total_tiles;
+  const int64_t smax = pm ? YANERF_DW_SMAX_PM : YANERF_DW_SMAX;
+  int64_t S = (smax * 64 + total_tiles - 1) / total_tiles;
   if (S > n_stages) S = n_stages;
-  if (S > YANERF_DW_SMAX) S = YANERF_DW_SMAX;
+  if (S > smax) S = smax;
   if (pm) {
     const int64_t cap = (int64_t)(Cfg<bf16_t>::M / PM_SPTS) * (PM_SCALES - 2);  // stages per split whose scales fit
     if (S < (n_stages + cap - 1) / cap) S = (n_stages + cap - 1) / cap;
@@ -2566,6 +2708,8 @@ static int dw_x0p(const MlpLayout& L, bool pm, const DwSpec& sp) {
   return (sp.x0_rows + q - 1) / q * q;
 }
 
+// a split's slab stride: whole 16-byte groups, so the reduce reads every split with aligned 16-byte loads
+static int64_t dw_slab_pad(int64_t e) { return (e + 3) / 4 * 4; }
 static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void* gradbuf, int64_t Npad,
                           float* const* grads, DwJobs& D) {
   const size_t es = elem_size(prec);
@@ -2629,6 +2773,7 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     j.W = grads[sp.gi];
     j.b = grads[sp.gi + 1];
   });
+  D.slab_stride = dw_slab_pad(D.slab_elems);
 }
 
 static int64_t dw_slab_elems_for(const MlpLayout& L, int prec, int* total_tiles) {
@@ -2644,7 +2789,7 @@ static int64_t dw_slab_elems_for(const MlpLayout& L, int prec, int* total_tiles)
     tiles += kt;
   });
   if (total_tiles) *total_tiles = tiles;
-  return e;
+  return dw_slab_pad(e);
 }
 
 // dW kernel type and precision per mode: x3 saves fp32 activations / gradients, so its weight gradients run on
@@ -2714,7 +2859,7 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
     YN_LAUNCH_CHECK("mlp_backward_dw");
   }
   if (red) {
-    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((D.slab_elems + 255) / 256)), dim3(256), 0, st, D, S, slab);
+    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((D.slab_elems + 1023) / 1024)), dim3(256), 0, st, D, S, slab);
     YN_LAUNCH_CHECK("mlp_backward_reduce");
   }
   return 0;

@@ -583,11 +583,16 @@ __device__ __forceinline__ void mma_grid(const f4 (&a)[NI], const f4 (&b)[NJ], f
 // bf16 weight-fragment ring (see gemm_lds). A caller may fill it for the NEXT GEMM before running the current
 // layer's epilogue, so that GEMM starts on weights already in registers instead of an L2 round trip.
 template <typename T, int NT> struct ARing { f4 a[Cfg<T>::APREF][Cfg<T>::PLANES][NT]; };
-template <typename T, int NT>
+template <typename T, int NT, bool OPQ = false>
 __device__ __forceinline__ void ring_fill(ARing<T, NT>& R, const typename Cfg<T>::w_t* __restrict__ W, int64_t wplane,
                                           int ldw, int nrow0, int nkb, int lane) {
   if constexpr (sizeof(typename Cfg<T>::w_t) == 2) {
     constexpr int D = Cfg<T>::APREF, EPC = Cfg<T>::EPC, KB = Cfg<T>::KB, FRAG = 64 * EPC, NP = Cfg<T>::PLANES;
+    // OPQ (the dX layer loop): an opaque lane id, as in gemm_run, so the per-lane weight base is recomputed per fill
+    // instead of being hoisted out of the loop and spilled -- the bf16 dX reloaded it every layer, and the scratch
+    // reload waited (shared in-order vmcnt) for all of the wave's gradient-row stores: dX 1.01 -> 0.935 ms. (The
+    // forward keeps the hoisted base: opaque there it measured 0.94 -> 0.96 ms.)
+    if constexpr (OPQ) asm volatile("" : "+v"(lane));
 #pragma unroll
     for (int r = 0; r < D; ++r) {
       const int k = (YANERF_ABLATE & 256) ? 0 : (r < nkb ? r : nkb - 1);
@@ -1185,10 +1190,25 @@ __device__ __forceinline__ void save_relu_pm(const typename Cfg<T>::lds_t* act, 
 // operands only. Each leaves a tile as fp8 e4m3 of value / s with one power-of-two s per (section, 128-point tile),
 // chosen so the tile's largest |value| lands in [128, 256) (below e4m3's 448 after the bf16 rounding of the LDS copy);
 // s goes to a small scale array beside the rows and the dW tile widens the fragments with it (exact).
+// max over the wave without address registers: DPP within each 16-lane row (quad xor 1, xor 2, half-row mirror,
+// row mirror), then the four rows through readlane (the result is wave-uniform). A __shfl_xor form needs six
+// ds_bpermute address VGPRs, which the compiler hoisted out of the dX layer loop and spilled: every reload then
+// waited (shared in-order vmcnt) for all of the wave's outstanding gradient-row stores.
+template <int CTRL>
+__device__ __forceinline__ float dpp_fmax(float v) {
+  const int o = __builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xf, 0xf, false);
+  return fmaxf(v, __int_as_float(o));
+}
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = dpp_fmax<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v = dpp_fmax<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v = dpp_fmax<0x141>(v);  // row_half_mirror
+  v = dpp_fmax<0x140>(v);  // row_mirror
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
 // running |max| of packed bf16 tile values as two u16 maxima of the magnitude bits (one VGPR, two VALU per chunk)
 struct G8Max {
@@ -1595,7 +1615,7 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
   // ---- dY = Wc[:, :256]^T dZc   (K = 128)
   gemm_lds<T, NT, MT>(Wt + lay.wcT_off, wpl, HC, nrow0, act, 0, HC / KB, acc, lane);
   ARing<T, NT> ring;  // next GEMM's weights, fetched during the epilogue (bf16)
-  ring_fill<T, NT>(ring, Wt + lay.wintT_off, wpl, 256, nrow0, 256 / KB, lane);
+  ring_fill<T, NT, true>(ring, Wt + lay.wintT_off, wpl, 256, nrow0, 256 / KB, lane);
   // point-major gradients leave the LDS tile after the GEMM that reads them (and its next-ring loads): see the
   // forward's trunk loop on the shared, in-order vmcnt
   if constexpr (PM)
@@ -1632,7 +1652,7 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
     for (int w = 0; w < MW; ++w)
       bits[w] = masks[((((int64_t)hl * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane];
     gemm_lds<T, NT, MT>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring);
-    if (l - 1 >= 1) ring_fill<T, NT>(ring, Wt + lay.wt_off[l - 1], wpl, 256, nrow0, 256 / KB, lane);
+    if (l - 1 >= 1) ring_fill<T, NT, true>(ring, Wt + lay.wt_off[l - 1], wpl, 256, nrow0, 256 / KB, lane);
     // fp8 scale sets: dZc 0, dY 1, then dZ_{L-1}, dZ_{L-2}, ... alternate from set 0
     if constexpr (PM && !(YANERF_ABLATE & 128)) {  // the GEMM's input: dY (from the heads) or dZ_l
       if constexpr (HEAD)

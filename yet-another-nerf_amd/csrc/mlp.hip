@@ -1529,6 +1529,11 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
   const int64_t p = p0 + mt_;
   const bool valid = p < N;
   const int cd = lay.cdim;
+  // fp32 slot i of the heads-step staging (w_d at 0..255, dsigma at 256 + point) in the PE columns of rows 20.. (the
+  // dX kernel's GEMMs never read the PE columns; rows 0..15 hold the colour-output weights, row 16 the fp8 scale slots)
+  constexpr int HFPR = KPE * (int)sizeof(LT) / 4;  // fp32 slots per row
+  static_assert(20 + (256 + M) / HFPR <= M, "heads-step staging rows");
+  auto hd_lds = [&](int i) -> float* { return (float*)(act + (20 + i / HFPR) * ROW + PE_COL) + (i % HFPR); };
   // ---- sigmoid backward (grad * (1 - y) * y) and output layer backward
   float du[CMAX] = {0.f, 0.f, 0.f, 0.f};
   const float gs = valid ? g_sigma[p] : 0.0f;
@@ -1538,16 +1543,19 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
       du[j] = (g_rgb[p * cd + j] * (1.0f - y)) * y;
     }
   }
-  if (q == 0) {
-    if constexpr (PM) {
-      ST* gdu = (ST*)(gb + PG.du) + p * 16;
-      for (int j = 0; j < cd; ++j) gdu[j] = to_st<T>(du[j]);
-      gdu[PM_DSIG] = to_st<T>(gs);
-    } else {
-      for (int j = 0; j < cd; ++j) grad[(GR.du + j) * ld + p] = to_st<T>(du[j]);
-      grad[(GR.dyx + 256) * ld + p] = to_st<T>(gs);
+  // dU / dsigma rows: stored after the colour head (below), whose mask-word loads would otherwise wait for them
+  auto store_du = [&]() {
+    if (q == 0) {
+      if constexpr (PM) {
+        ST* gdu = (ST*)(gb + PG.du) + p * 16;
+        for (int j = 0; j < cd; ++j) gdu[j] = to_st<T>(du[j]);
+        gdu[PM_DSIG] = to_st<T>(gs);
+      } else {
+        for (int j = 0; j < cd; ++j) grad[(GR.du + j) * ld + p] = to_st<T>(du[j]);
+        grad[(GR.dyx + 256) * ld + p] = to_st<T>(gs);
+      }
     }
-  }
+  };
   {
     // the colour-output weights (cd x HC fp32, <= 2 KB) are staged once in the LDS tile's PE columns, which the dX
     // kernel never uses: the colour-head backward then reads them as 16-byte LDS broadcasts (the lanes of one point
@@ -1557,6 +1565,10 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
     static_assert(WFPR % 8 == 0 && (CMAX * HC) / WFPR <= M, "colour-output weights in the PE columns");
     auto wo_row = [&](int i) -> float* { return (float*)(act + (i / WFPR) * ROW + PE_COL) + (i % WFPR); };
     for (int i = tid; i < CMAX * HC; i += NTHR) *wo_row(i) = i < cd * HC ? Wf[lay.wo_off + i] : 0.0f;
+    // the density-head weights w_d and this tile's dsigma, for the heads step's w_d (x) dsigma term (read there from
+    // LDS: as global loads after the dY stores, each waited on the in-order vmcnt for those stores)
+    for (int i = tid; i < 256; i += NTHR) hd_lds(i)[0] = Wf[lay.wd_off + i];
+    if (q == 0) hd_lds(256 + mt_)[0] = gs;
     // colour-hidden ReLU masks for this point: feature tiles CPT/16 * q .. (slot L)
     constexpr int TT = CPT / 16;
     uint64_t cw[TT][4];
@@ -1609,6 +1621,7 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
       }
     g8_note(0, amax);  // dZc: set 0
   }
+  store_du();
   lds_barrier();
   f4 acc[NT][MT];
   const int nrow0 = wave * NT * 16;
@@ -1667,13 +1680,13 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
     for (int nt = 0; nt < NT; ++nt) {
       const int n = nrow0 + 16 * nt + 4 * g;
       f4 wdv = f4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (HEAD) wdv = *(const f4*)(Wf + lay.wd_off + n);
+      if constexpr (HEAD) wdv = *(const f4*)hd_lds(n);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int m = 16 * mt + li;
         f4 v = acc[nt][mt];
         if constexpr (HEAD) {
-          const float gsm = (p0 + m < N) ? g_sigma[p0 + m] : 0.0f;
+          const float gsm = *hd_lds(256 + m);  // 0 past N (gs of an invalid point)
           v = v + wdv * gsm;
         }
         // ReLU mask of H_{hl}: this lane's own bits of this tile (packed by the forward)

@@ -399,48 +399,62 @@ struct PackJobs {
   int64_t total;
 };
 
+// One thread per 4 consecutive columns of one row of a job (every job's cols is a multiple of 4, so a group never
+// straddles jobs or rows, and in fragment order its 4 outputs are contiguous: c % EPC runs over an aligned 4 of EPC).
 template <typename T>
 __global__ void pack_kernel(PackJobs jobs, typename Cfg<T>::w_t* __restrict__ dst_t, float* __restrict__ dst_f,
                             int64_t t_plane) {
-  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= jobs.total) return;
+  const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (e0 >= jobs.total) return;
   int lo = 0, hi = jobs.n - 1;
   while (lo < hi) {
     int mid = (lo + hi + 1) >> 1;
-    if (jobs.j[mid].elem_base <= e) lo = mid; else hi = mid - 1;
+    if (jobs.j[mid].elem_base <= e0) lo = mid; else hi = mid - 1;
   }
   const PackJob& J = jobs.j[lo];
-  int64_t local = e - J.elem_base;
-  int r = (int)(local / J.cols), c = (int)(local % J.cols);
-  int n = J.transpose ? c : r;  // output-feature index
-  int k = J.transpose ? r : c;  // input-feature index (packed column)
-  int sk = -1;
-  if (k < J.seg0) sk = k;
-  else if (k >= J.seg1_start && k < J.seg1_start + J.seg1_len) sk = J.seg0 + (k - J.seg1_start);
-  float v = 0.0f;
-  if (sk >= 0 && n < J.src_rows) v = J.src[(int64_t)n * J.src_ld + sk];
+  const int64_t local0 = e0 - J.elem_base;
+  const int r = (int)(local0 / J.cols), c0 = (int)(local0 % J.cols);
+  float v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = c0 + i;
+    const int n = J.transpose ? c : r;  // output-feature index
+    const int k = J.transpose ? r : c;  // input-feature index (packed column)
+    int sk = -1;
+    if (k < J.seg0) sk = k;
+    else if (k >= J.seg1_start && k < J.seg1_start + J.seg1_len) sk = J.seg0 + (k - J.seg1_start);
+    v[i] = (sk >= 0 && n < J.src_rows) ? J.src[(int64_t)n * J.src_ld + sk] : 0.0f;
+  }
   if (J.is_f32) {
-    dst_f[J.dst_off + local] = v;
-  } else {
-    // GEMM operands are stored in MFMA A-fragment order: for each 16-row tile and 64-byte K-block, 64 lanes x 16 B,
-    // lane = 16 * (k-chunk) + (row within the tile), so one wave-wide 16-byte load reads 1 KiB contiguously
-    constexpr int KB = Cfg<T>::KB, EPC = Cfg<T>::EPC;
-    const int64_t fi = (((int64_t)(r >> 4) * (J.cols / KB) + c / KB) * 64 + ((c % KB) / EPC) * 16 + (r & 15)) * EPC +
-                       c % EPC;
-    if constexpr (is_x3<T>) {
-      // three bf16 planes, x = x0 + x1 + x2 exactly (each residual is exact in fp32)
-      const bf16_t x0 = f2bf(v);
-      const float r1 = v - bf2f(x0);
-      const bf16_t x1 = f2bf(r1);
-      const bf16_t x2 = f2bf(r1 - bf2f(x1));
-      dst_t[J.dst_off + fi] = x0;
-      dst_t[t_plane + J.dst_off + fi] = x1;
-      dst_t[2 * t_plane + J.dst_off + fi] = x2;
-    } else if constexpr (sizeof(T) == 4) {
-      dst_t[J.dst_off + fi] = v;
-    } else {
-      dst_t[J.dst_off + fi] = f2bf(v);
+    *(f4*)(dst_f + J.dst_off + local0) = f4{v[0], v[1], v[2], v[3]};
+    return;
+  }
+  // GEMM operands are stored in MFMA A-fragment order: for each 16-row tile and 64-byte K-block, 64 lanes x 16 B,
+  // lane = 16 * (k-chunk) + (row within the tile), so one wave-wide 16-byte load reads 1 KiB contiguously
+  constexpr int KB = Cfg<T>::KB, EPC = Cfg<T>::EPC;
+  const int64_t fi = (((int64_t)(r >> 4) * (J.cols / KB) + c0 / KB) * 64 + ((c0 % KB) / EPC) * 16 + (r & 15)) * EPC +
+                     c0 % EPC;
+  if constexpr (is_x3<T>) {
+    // three bf16 planes, x = x0 + x1 + x2 exactly (each residual is exact in fp32)
+    bf16_t x[3][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x[0][i] = f2bf(v[i]);
+      const float r1 = v[i] - bf2f(x[0][i]);
+      x[1][i] = f2bf(r1);
+      x[2][i] = f2bf(r1 - bf2f(x[1][i]));
     }
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+      const uint2 w = {(uint32_t)x[pl][0] | ((uint32_t)x[pl][1] << 16), (uint32_t)x[pl][2] | ((uint32_t)x[pl][3] << 16)};
+      *(uint2*)(dst_t + pl * t_plane + J.dst_off + fi) = w;
+    }
+  } else if constexpr (sizeof(T) == 4) {
+    *(f4*)(dst_t + J.dst_off + fi) = f4{v[0], v[1], v[2], v[3]};
+  } else {
+    const uint2 w = {(uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                     (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)};
+    *(uint2*)(dst_t + J.dst_off + fi) = w;
   }
 }
 
@@ -2629,7 +2643,7 @@ static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, const f
     j.src = src; j.src_rows = src_rows; j.src_ld = src_ld; j.dst_off = dst_off; j.rows = rows; j.cols = cols;
     j.seg0 = seg0; j.seg1_start = seg1_start; j.seg1_len = seg1_len; j.transpose = transpose; j.is_f32 = is_f32;
     j.elem_base = J.total;
-    J.total += (int64_t)rows * cols;
+    J.total += (int64_t)rows * cols;  // cols % 4 == 0 for every job (pack_kernel's 4-column groups)
   };
   const int nl = L.L;
   for (int l = 0; l < nl; ++l) {
@@ -2925,7 +2939,7 @@ int yanerf_mlp_pack(const yanerf_mlp_desc* d, int precision, const float* const*
   build_pack_jobs(d, L, params, J);
   char* base = (char*)packed;
   float* fsec = (float*)(base + L.f_base);
-  dim3 grid((unsigned)((J.total + 255) / 256)), block(256);
+  dim3 grid((unsigned)((J.total / 4 + 255) / 256)), block(256);
   if (precision == YANERF_PREC_F32)
     hipLaunchKernelGGL(pack_kernel<float>, grid, block, 0, as_stream(stream), J, (float*)base, fsec, L.t_plane);
   else if (precision == YANERF_PREC_BF16)

@@ -1804,6 +1804,18 @@ constexpr bool DW_PF = YANERF_DW_PF;  // fp32 dW: prefetch the next stage's frag
 #define YANERF_DW_STAGES (YANERF_DW_CPR == 4 ? 4 : 2)
 #endif
 constexpr int DW_STAGES = YANERF_DW_STAGES, DW_STAGE_BYTES = 512 * DW_RB;
+// fp32 ring: a stage holds at most 256 + 128 rows (dw_bkmax 128), 4 stages = 96 KB. (3 stages = 72 KB let two
+// workgroups share a CU -- 16 waves, 4 per SIMD, at the tile's 116 VGPRs -- and measured slower: fp32 dW 8.15 ->
+// 8.33 ms; the fp32 dW's idle MFMA cycles are not stage-barrier bubbles another workgroup could fill.)
+#ifndef YANERF_DW32_STAGES
+#define YANERF_DW32_STAGES 4
+#endif
+template <typename T> struct DwRing {
+  static constexpr int STAGES = DW_STAGES, STAGE_BYTES = DW_STAGE_BYTES;
+};
+template <> struct DwRing<float> {
+  static constexpr int STAGES = YANERF_DW32_STAGES, STAGE_BYTES = (256 + 128) * DW_RB;
+};
 // points per dW stage: one K-block of the dW MFMA per staged row (x3: always one bf16 K-block, register staged)
 constexpr int X3_SPTS = 32;
 static int64_t dw_stage_pts(int prec) {
@@ -1819,9 +1831,11 @@ template <typename T, int BN, int BK>
 __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, int64_t Npad, float* __restrict__ slab,
                                         int64_t slab_elems, char* smem) {
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
+  constexpr int RSTG = DwRing<T>::STAGES, RSB = DwRing<T>::STAGE_BYTES;  // ring depth, bytes per stage
   constexpr int WN = BN / 64, WK0 = 8 / WN, WK = (BK / 16 < WK0) ? BK / 16 : WK0, KTW = BK / WK / 16;
   static_assert(KTW >= 1 && WN * WK <= 8, "dW wave tiling");
   constexpr int ROWS = BN + BK, PW = (ROWS + 8 * DW_RPI - 1) / (8 * DW_RPI);  // DMA wave-instrs per wave per stage
+  static_assert(PW * 8 * 1024 <= RSB, "dW stage buffer");
   constexpr int KBS = DW_CPR / 4;                                             // K-blocks per stage
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1849,7 +1863,7 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
     src[i] = p + ch * EPC;
   }
   auto issue = [&](int64_t st) {
-    char* dst = smem + (int)(st % DW_STAGES) * DW_STAGE_BYTES;
+    char* dst = smem + (int)(st % RSTG) * RSB;
 #pragma unroll
     for (int i = 0; i < PW; ++i)
       __builtin_amdgcn_global_load_lds(src[i] + st * (KB * KBS),
@@ -1876,9 +1890,9 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
   if constexpr (DW_PF && KBS == 1) {
     // Fragment prefetch: the wave reads stage st+1's MFMA fragments from LDS while it multiplies stage st's (held
     // in registers since the previous iteration), so no stage starts on an LDS read latency. Stage st+1 must have
-    // landed at iteration st's barrier; the DMA issued after it (stage st + DW_STAGES - 1) fills buffer
-    // (st-1) % DW_STAGES, whose fragments were read at iteration st-2 and whose bias rows at iteration st-1.
-    static_assert(DW_STAGES >= 3, "prefetch ring");
+    // landed at iteration st's barrier; the DMA issued after it (stage st + RSTG - 1) fills buffer
+    // (st-1) % RSTG, whose fragments were read at iteration st-2 and whose bias rows at iteration st-1.
+    static_assert(RSTG >= 3, "prefetch ring");
     constexpr int NB = KTW;
     f4 a[2][4], b[2][NB];
     auto read_frags = [&](const char* buf, f4 (&fa)[4], f4 (&fb)[NB]) {
@@ -1912,12 +1926,12 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
     };
     int64_t ihi = st_lo;  // next stage to issue
 #pragma unroll
-    for (int i = 0; i < DW_STAGES - 1; ++i)
+    for (int i = 0; i < RSTG - 1; ++i)
       if (ihi < st_hi) issue(ihi++);
     if (st_lo < st_hi) {
       wait_dma(ihi - 1 - st_lo);
       __builtin_amdgcn_s_barrier();
-      if (mma_wave) read_frags(smem + (int)(st_lo % DW_STAGES) * DW_STAGE_BYTES, a[0], b[0]);
+      if (mma_wave) read_frags(smem + (int)(st_lo % RSTG) * RSB, a[0], b[0]);
     }
     // two stages per trip so the fragment buffers alternate without register copies
     for (int64_t st = st_lo; st < st_hi; st += 2) {
@@ -1930,28 +1944,28 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
           if (ihi < st_hi) issue(ihi++);
-          if (has_next && mma_wave) read_frags(smem + (int)((sc + 1) % DW_STAGES) * DW_STAGE_BYTES, a[h ^ 1], b[h ^ 1]);
+          if (has_next && mma_wave) read_frags(smem + (int)((sc + 1) % RSTG) * RSB, a[h ^ 1], b[h ^ 1]);
           mma(a[h], b[h]);
-          if (do_bias) bias_rows(smem + (int)(sc % DW_STAGES) * DW_STAGE_BYTES);
+          if (do_bias) bias_rows(smem + (int)(sc % RSTG) * RSB);
         }
       }
     }
   } else {
 #pragma unroll
-  for (int i = 0; i < DW_STAGES - 1; ++i)
+  for (int i = 0; i < RSTG - 1; ++i)
     if (st_lo + i < st_hi) issue(st_lo + i);
   for (int64_t st = st_lo; st < st_hi; ++st) {
     // my DMA for stage st is complete once at most the later issued stages remain outstanding
-    const int64_t ahead = st_hi - 1 - st;  // stages issued after st (at most DW_STAGES - 2 here)
-    static_assert(DW_STAGES >= 2 && DW_STAGES <= 5, "wait ladder below");
-    if (ahead >= DW_STAGES - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (DW_STAGES - 2)) : "memory");
-    else if (DW_STAGES == 5 && ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * 2) : "memory");
+    const int64_t ahead = st_hi - 1 - st;  // stages issued after st (at most RSTG - 2 here)
+    static_assert(RSTG >= 2 && RSTG <= 5, "wait ladder below");
+    if (ahead >= RSTG - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (RSTG - 2)) : "memory");
+    else if (RSTG == 5 && ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * 2) : "memory");
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (st + DW_STAGES - 1 < st_hi) issue(st + DW_STAGES - 1);
-    const char* buf = smem + (int)(st % DW_STAGES) * DW_STAGE_BYTES;
+    if (st + RSTG - 1 < st_hi) issue(st + RSTG - 1);
+    const char* buf = smem + (int)(st % RSTG) * RSB;
 #pragma unroll
     for (int kb = 0; kb < KBS; ++kb)
     if (mma_wave) {
@@ -2534,7 +2548,7 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   // x3: two buffers of three 384-row bf16 planes (144 KB); otherwise the LDS-DMA ring
   __shared__ __attribute__((aligned(16))) char smem[is_x3<T>      ? 2 * 3 * 384 * 64
                                                     : Cfg<T>::PM ? PM_STAGES * PM_STAGE_BYTES + 2 * PM_SCALES * 4
-                                                                 : DW_STAGES * DW_STAGE_BYTES];
+                                                                 : DwRing<T>::STAGES * DwRing<T>::STAGE_BYTES];
   // 1-D grid in job order (heaviest first); inside a job, split-major so the k-tiles sharing a dZ slab run together.
   // (An XCD-aware order -- the tiles of jobs that share a section as consecutive blocks of one XCD -- measured slower:
   // bf16 dW 1.175 -> 1.21 ms, fp32 8.23 -> 9.10 ms.)
@@ -2585,16 +2599,16 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
       dw_tile_x3<64, 128>(J, k0, s, S, Npad, slab, se, smem);
     }
   } else if (J.bn == 256) {
-    if (bk == 256) dw_tile<T, 256, 256>(J, k0, s, S, Npad, slab, se, smem);
-    else if (bk == 128) dw_tile<T, 256, 128>(J, k0, s, S, Npad, slab, se, smem);
+    // (fp32 tiles are at most dw_bkmax = 128 wide: no 256-column instantiations, whose 128 accumulators per wave would
+    // set the whole kernel's VGPR count)
+    static_assert(BKMAX == 128, "fp32 dW tiles");
+    if (bk == 128) dw_tile<T, 256, 128>(J, k0, s, S, Npad, slab, se, smem);
     else dw_tile<T, 256, 64>(J, k0, s, S, Npad, slab, se, smem);
   } else if (J.bn == 128) {
-    if (bk == 256) dw_tile<T, 128, 256>(J, k0, s, S, Npad, slab, se, smem);
-    else if (bk == 128) dw_tile<T, 128, 128>(J, k0, s, S, Npad, slab, se, smem);
+    if (bk == 128) dw_tile<T, 128, 128>(J, k0, s, S, Npad, slab, se, smem);
     else dw_tile<T, 128, 64>(J, k0, s, S, Npad, slab, se, smem);
   } else {
-    if (bk == 256) dw_tile<T, 64, 256>(J, k0, s, S, Npad, slab, se, smem);
-    else dw_tile<T, 64, 128>(J, k0, s, S, Npad, slab, se, smem);
+    dw_tile<T, 64, 128>(J, k0, s, S, Npad, slab, se, smem);
   }
 }
 

@@ -151,6 +151,19 @@ int yanerf_composite_backward(const yanerf_raymarch_opts* o, const float* sigma_
                               const float* g_alpha, int64_t R, int64_t P, int64_t C, float* g_sigma,
                               float* g_rgb, void* stream);
 
+/* The fused trainer's per-pass composite: yanerf_composite_forward, yanerf_rgb_loss (L = scale * sum((features -
+ * gt)^2), gt gathered from image [B][H][W][C] at xys [R][2], R / B rays per image) and yanerf_composite_backward from
+ * dL/dfeatures (no depth / alpha gradient) in one launch, bit-identical to those three calls; replaces
+ * EmissionAbsorptionRaymarcher.forward + the rgb_mse term + their autograd backward on the training step
+ * (renderer.py:146-278; pipelines/utils.py:189-196; nerf_pipeline.py:284-305). sq_err_per_ray and g_features
+ * (the loss's intermediate values) may be NULL. */
+int yanerf_composite_train(const yanerf_raymarch_opts* o, const float* sigma_raw, const float* rgb,
+                           const float* lengths, const float* directions, const float* bg, const float* noise,
+                           const float* image, const float* xys, int64_t B, int64_t R, int64_t P, int64_t C,
+                           int64_t H, int64_t W, float scale, float* features, float* depths, float* alpha,
+                           float* weights, float* sq_err_per_ray, float* g_features, float* g_sigma, float* g_rgb,
+                           void* stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Importance sampling (sample_pdf_python, yanerf/pipelines/renderers/utils.py:83-158) and the
  * refiner (RayPointRefiner.forward, renderers/utils.py:48-69).

@@ -134,6 +134,33 @@ def test_trainer_step_matches_registry_step(golden, precision):
             np.testing.assert_allclose(b, a, atol=tol, err_msg=f"model {i} {name}")
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_fused_composite_matches_three_launches(precision):
+    """yanerf_composite_train (composite forward + photometric loss + composite backward in one launch per pass) is
+    bit-identical to yanerf_composite_forward + yanerf_rgb_loss + yanerf_composite_backward: two trainers with the
+    same weights and Philox stream (density noise on) take two steps each; losses, features, weights, the flat
+    gradient and the updated parameters must be equal bit for bit."""
+    from scene import synthetic_pose
+    trs = [make_trainer(precision, (11, 12), n_rays=512) for _ in range(2)]
+    trs[1].fused_composite = False
+    g = torch.Generator().manual_seed(3)
+    img = torch.rand(1, 800, 800, 3, generator=g).to(DEV)
+    outs = []
+    for tr in trs:
+        res = []
+        for k in range(2):
+            pose = torch.from_numpy(synthetic_pose(30.0 * k, -30.0, 4.0)).float()[None].to(DEV)
+            out = tr.step(pose, torch.tensor([1111.111], device=DEV), img)
+            torch.cuda.synchronize()
+            res.append([out["sq_coarse"].clone(), out["sq_fine"].clone(), tr.flat.grad.clone(),
+                        tr.passes[0].feats.clone(), tr.passes[1].w.clone(), tr.passes[1].g_sigma.clone()])
+        res.append([tr.flat.data.clone()])
+        outs.append(res)
+    for a, b in zip(*outs):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+
+
 def test_trainer_lr_schedule_and_adam_state():
     """With the runner config the fused step uses the reference schedule at passed_iter = steps taken (decay, then
     warm-up; apis.py:66-68), and the Adam step count advances as torch's state['step']."""

@@ -20,7 +20,8 @@ PREC_F32X3 = 2  # fp32 as three bf16 terms, six bf16 MFMAs per product (include/
 EXPORTS = (
     "yanerf_last_error", "yanerf_version", "yanerf_raygen", "yanerf_mlp_num_params", "yanerf_mlp_packed_bytes",
     "yanerf_mlp_pack", "yanerf_mlp_saved_bytes", "yanerf_mlp_bwd_workspace_bytes", "yanerf_mlp_forward",
-    "yanerf_mlp_backward", "yanerf_mlp_backward_phase", "yanerf_composite_forward", "yanerf_composite_backward", "yanerf_sample_pdf",
+    "yanerf_mlp_backward", "yanerf_mlp_backward_phase", "yanerf_composite_forward", "yanerf_composite_backward",
+    "yanerf_composite_train", "yanerf_sample_pdf",
     "yanerf_refine", "yanerf_rgb_loss", "yanerf_adam",
 )
 
@@ -78,6 +79,8 @@ def lib():
         "yanerf_composite_forward": (c_int, [POINTER(RaymarchOpts), P, P, P, P, P, P, i64, i64, i64, P, P, P, P, P]),
         "yanerf_composite_backward": (c_int, [POINTER(RaymarchOpts), P, P, P, P, P, P, P, P, P, i64, i64, i64, P, P,
                                               P]),
+        "yanerf_composite_train": (c_int, [POINTER(RaymarchOpts), P, P, P, P, P, P, P, P, i64, i64, i64, i64, i64,
+                                           i64, c_float, P, P, P, P, P, P, P, P, P]),
         "yanerf_sample_pdf": (c_int, [P, P, i64, i64, i64, c_int, P, c_uint64, c_uint64, P, P]),
         "yanerf_refine": (c_int, [P, P, i64, i64, i64, c_int, P, c_uint64, c_uint64, c_int, P, P]),
         "yanerf_rgb_loss": (c_int, [P, P, P, i64, i64, i64, i64, i64, c_float, P, P, P]),

@@ -155,14 +155,29 @@ __device__ __forceinline__ float noise_at(const yanerf_raymarch_opts& o, const f
 __device__ __forceinline__ float cap_fn(int kind, float x) { return kind == 0 ? 1.0f - expf(-x) : fminf(x, 1.0f); }
 __device__ __forceinline__ float cap_grad(int kind, float x) { return kind == 0 ? expf(-x) : (x <= 1.0f ? 1.0f : 0.0f); }
 
-template <bool BACKWARD>
+// the photometric loss of the fused training composite (MODE 2): rgb_loss_kernel's arithmetic on the ray's features
+struct CompositeLoss {
+  const float* image;  // [B][H][W][C]
+  const float* xys;    // [B * rays_per_image][2]
+  int64_t rays_per_image, H, W;
+  float scale;
+  float* sq;      // [R] per-ray squared error (may be null)
+  float* g_feat;  // [R][C] dL/dfeatures (may be null)
+};
+
+// MODE 0: forward (features, depths, alpha, weights); 1: backward from g_features / g_depths / g_alpha; 2: the training
+// pass of the fused trainer in one launch -- the forward outputs, the loss of the features against the image
+// (rgb_loss_kernel's arithmetic, on lane 0's features as the separate kernels see them) and the backward from that
+// gradient (g_depths = g_alpha = 0), bit-identical to the three launches it replaces
+template <int MODE>
 __global__ void __launch_bounds__(256) composite_kernel(
     yanerf_raymarch_opts o, const float* __restrict__ sigma_raw, const float* __restrict__ rgb,
     const float* __restrict__ lengths, const float* __restrict__ dirs, const float* __restrict__ bg,
     const float* __restrict__ noise, int64_t R, int64_t P, int64_t C, float* __restrict__ features,
     float* __restrict__ depths, float* __restrict__ alpha_out, float* __restrict__ weights_out,
     const float* __restrict__ g_features, const float* __restrict__ g_depths, const float* __restrict__ g_alpha,
-    float* __restrict__ g_sigma, float* __restrict__ g_rgb) {
+    float* __restrict__ g_sigma, float* __restrict__ g_rgb, CompositeLoss loss) {
+  constexpr bool BACKWARD = MODE == 1;
   const int lane = threadIdx.x & 63;
   const int64_t ray = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (ray >= R) return;
@@ -241,6 +256,7 @@ __global__ void __launch_bounds__(256) composite_kernel(
   for (int c = 0; c < C && c < 4; ++c)
     bgc[c] = bg ? bg[ray * C + c] : (o.bg_default_n == 1 ? o.bg_default[0] : o.bg_default[c]);
 
+  float gL[4] = {0, 0, 0, 0};  // MODE 2: dL/dfeatures
   if (!BACKWARD) {
     float dep = 0.0f, F[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -270,13 +286,31 @@ __global__ void __launch_bounds__(256) composite_kernel(
         features[ray * C + c] = f;
       }
     }
-    return;
+    if constexpr (MODE == 0) return;
+    // loss (rgb_loss_kernel): lane 0's features, as the separate kernels read them back
+    const int64_t b = ray / loss.rays_per_image;
+    const int64_t x = (int64_t)loss.xys[ray * 2 + 0], y = (int64_t)loss.xys[ray * 2 + 1];
+    const float* px = loss.image + ((b * loss.H + y) * loss.W + x) * C;
+    float sq = 0.0f;
+    for (int c = 0; c < C && c < 4; ++c) {
+      float f = F[c];
+      if (!o.hard_background) {
+        float A = o.blend_output ? alpha : 1.0f;
+        f = A * F[c] + (1.0f - alpha) * bgc[c];
+      }
+      f = __shfl(f, 0, 64);
+      const float d = f - px[c];
+      sq += d * d;
+      gL[c] = loss.scale * 2.0f * d;
+      if (lane == 0 && loss.g_feat) loss.g_feat[ray * C + c] = gL[c];
+    }
+    if (lane == 0 && loss.sq) loss.sq[ray] = sq;
   }
 
   // -------- backward
   float gF[4] = {0, 0, 0, 0};
-  float gD = g_depths ? g_depths[ray] : 0.0f;
-  float gA = g_alpha ? g_alpha[ray] : 0.0f;
+  float gD = (MODE == 1 && g_depths) ? g_depths[ray] : 0.0f;
+  float gA = (MODE == 1 && g_alpha) ? g_alpha[ray] : 0.0f;
   float g_op_last = gA;
   float Fsum[4] = {0, 0, 0, 0};
   if (!o.hard_background && o.blend_output) {
@@ -290,7 +324,7 @@ __global__ void __launch_bounds__(256) composite_kernel(
     for (int c = 0; c < C && c < 4; ++c) Fsum[c] = wave_sum(Fsum[c]);
   }
   for (int c = 0; c < C && c < 4; ++c) {
-    float g = g_features[ray * C + c];
+    float g = MODE == 2 ? gL[c] : g_features[ray * C + c];
     if (!o.hard_background) {
       float A = o.blend_output ? alpha : 1.0f;
       gF[c] = g * A;
@@ -599,9 +633,9 @@ int yanerf_composite_forward(const yanerf_raymarch_opts* o, const float* sigma_r
   if (composite_common(o, R, P, C)) return 1;
   YN_CHECK(o->noise_mode != 1 || noise, "composite: noise_mode 1 needs noise");
   if (R == 0) return 0;
-  hipLaunchKernelGGL(composite_kernel<false>, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, as_stream(stream), *o,
+  hipLaunchKernelGGL(composite_kernel<0>, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, as_stream(stream), *o,
                      sigma_raw, rgb, lengths, directions, bg, noise, R, P, C, features, depths, alpha, weights, nullptr,
-                     nullptr, nullptr, nullptr, nullptr);
+                     nullptr, nullptr, nullptr, nullptr, CompositeLoss{});
   YN_LAUNCH_CHECK("composite_forward");
   return 0;
 }
@@ -613,10 +647,30 @@ int yanerf_composite_backward(const yanerf_raymarch_opts* o, const float* sigma_
   if (composite_common(o, R, P, C)) return 1;
   YN_CHECK(g_features && g_sigma && g_rgb, "composite_backward: null gradient pointer");
   if (R == 0) return 0;
-  hipLaunchKernelGGL(composite_kernel<true>, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, as_stream(stream), *o,
+  hipLaunchKernelGGL(composite_kernel<1>, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, as_stream(stream), *o,
                      sigma_raw, rgb, lengths, directions, bg, noise, R, P, C, nullptr, nullptr, nullptr, nullptr,
-                     g_features, g_depths, g_alpha, g_sigma, g_rgb);
+                     g_features, g_depths, g_alpha, g_sigma, g_rgb, CompositeLoss{});
   YN_LAUNCH_CHECK("composite_backward");
+  return 0;
+}
+int yanerf_composite_train(const yanerf_raymarch_opts* o, const float* sigma_raw, const float* rgb,
+                           const float* lengths, const float* directions, const float* bg, const float* noise,
+                           const float* image, const float* xys, int64_t B, int64_t R, int64_t P, int64_t C,
+                           int64_t H, int64_t W, float scale, float* features, float* depths, float* alpha,
+                           float* weights, float* sq_err_per_ray, float* g_features, float* g_sigma, float* g_rgb,
+                           void* stream) {
+  YN_CHECK(B >= 1 && R % B == 0, "composite_train: %lld rays do not split over %lld images", (long long)R,
+           (long long)B);
+  if (composite_common(o, R, P, C)) return 1;
+  YN_CHECK(features && depths && alpha && weights && g_sigma && g_rgb && image && xys,
+           "composite_train: null pointer");
+  YN_CHECK(H > 0 && W > 0, "composite_train: image size %lld x %lld", (long long)H, (long long)W);
+  if (R == 0) return 0;
+  const CompositeLoss loss{image, xys, R / B, H, W, scale, sq_err_per_ray, g_features};
+  hipLaunchKernelGGL(composite_kernel<2>, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, as_stream(stream), *o,
+                     sigma_raw, rgb, lengths, directions, bg, noise, R, P, C, features, depths, alpha, weights,
+                     nullptr, nullptr, nullptr, g_sigma, g_rgb, loss);
+  YN_LAUNCH_CHECK("composite_train");
   return 0;
 }
 

@@ -135,6 +135,7 @@ class NeRFTrainer:
         self.param_ptrs = [_C.ptr_array([p.data_ptr() for p in ps]) for ps in self.params]
         self.events: Optional[Dict[str, List]] = None  # optional per-phase timing probes
         self.kernel_probes = False  # serialise the backward kernels (per-kernel timing; see step())
+        self.fused_composite = True  # yanerf_composite_train per pass (False: the three separate launches)
         # evaluation (full-grid rendering) settings of the same configs (ray_sampler.py:54-56; renderer.py:29-52)
         self.Pc_eval = int(rs.get("n_pts_per_ray_evaluation", self.Pc))
         self.Pn_eval = int(rd.get("n_pts_per_ray_fine_evaluation", self.Pn))
@@ -263,14 +264,23 @@ class NeRFTrainer:
                     o = self.march.opts(2, self.noise_std, seed, off)
             else:
                 o = self.march.opts(0, 0.0)
-            _C.check(L.yanerf_composite_forward(ctypes.byref(o), _p(ps.sigma), _p(ps.rgb), _p(z), _p(self.d), None,
-                                                _p(noise), R, P, C, _p(ps.feats), _p(ps.depth), _p(ps.alpha),
-                                                _p(ps.w), st), "yanerf_composite_forward")
-            _C.check(L.yanerf_rgb_loss(_p(ps.feats), _p(image), _p(self.xys), 1, R, self.H, self.W, C, scale,
-                                       _p(ps.sq), _p(ps.g_feats), st), "yanerf_rgb_loss")
-            _C.check(L.yanerf_composite_backward(ctypes.byref(o), _p(ps.sigma), _p(ps.rgb), _p(z), _p(self.d), None,
-                                                 _p(noise), _p(ps.g_feats), None, None, R, P, C, _p(ps.g_sigma),
-                                                 _p(ps.g_rgb), st), "yanerf_composite_backward")
+            if self.fused_composite:
+                # composite forward + photometric loss + composite backward in one launch (bit-identical to the three
+                # calls below, tests/test_gpu_trainer.py)
+                _C.check(L.yanerf_composite_train(ctypes.byref(o), _p(ps.sigma), _p(ps.rgb), _p(z), _p(self.d), None,
+                                                  _p(noise), _p(image), _p(self.xys), 1, R, P, C, self.H, self.W,
+                                                  scale, _p(ps.feats), _p(ps.depth), _p(ps.alpha), _p(ps.w),
+                                                  _p(ps.sq), _p(ps.g_feats), _p(ps.g_sigma), _p(ps.g_rgb), st),
+                         "yanerf_composite_train")
+            else:
+                _C.check(L.yanerf_composite_forward(ctypes.byref(o), _p(ps.sigma), _p(ps.rgb), _p(z), _p(self.d),
+                                                    None, _p(noise), R, P, C, _p(ps.feats), _p(ps.depth),
+                                                    _p(ps.alpha), _p(ps.w), st), "yanerf_composite_forward")
+                _C.check(L.yanerf_rgb_loss(_p(ps.feats), _p(image), _p(self.xys), 1, R, self.H, self.W, C, scale,
+                                           _p(ps.sq), _p(ps.g_feats), st), "yanerf_rgb_loss")
+                _C.check(L.yanerf_composite_backward(ctypes.byref(o), _p(ps.sigma), _p(ps.rgb), _p(z), _p(self.d),
+                                                     None, _p(noise), _p(ps.g_feats), None, None, R, P, C,
+                                                     _p(ps.g_sigma), _p(ps.g_rgb), st), "yanerf_composite_backward")
             out["sq_coarse" if k == 0 else "sq_fine"] = ps.sq
             if k == 0 and self.overlap == "early" and not self.kernel_probes:
                 # the coarse pass's loss and gradients are complete here and nothing of the fine pass depends on them:

@@ -423,6 +423,31 @@ __device__ float torch_row_sum(const float* x, int n) {
   return acc;
 }
 
+// torch_row_sum with its 32 partial-sum chains ps[k][l] on lanes 8k + l (each chain's adds in torch's order, so every
+// rounding is the same), combined as torch combines them: ps[0][l] += ps[1][l], ps[2][l], ps[3][l], then the tail
+// elements and ps[0][0..7] into one accumulator. Result on every lane. (One lane over the whole row: ~100 dependent
+// LDS reads per ray.)
+__device__ float torch_row_sum_wave(const float* x, int n, int lane) {
+  const int V = 8, nv = n / V, size_ilp = nv / 4;
+  const int k = (lane >> 3) & 3, l = lane & 7;
+  float v = 0.0f;
+  if (lane < 32) {
+    v = (size_ilp >= 1) ? x[k * V + l] : 0.0f;
+    for (int i = 1; i < size_ilp; ++i) v += x[(4 * i + k) * V + l];
+    if (k == 0)
+      for (int i = size_ilp * 4; i < nv; ++i) v += x[i * V + l];
+  }
+  const float p1 = __shfl(v, 8 + l, 64), p2 = __shfl(v, 16 + l, 64), p3 = __shfl(v, 24 + l, 64);
+  v = ((v + p1) + p2) + p3;  // ps[0][l] on lanes 0..7
+  float acc = 0.0f;
+  for (int kk = nv * V; kk < n; ++kk) acc += x[kk];
+  if (nv > 0) {
+#pragma unroll
+    for (int ll = 0; ll < 8; ++ll) acc += __shfl(v, ll, 64);
+  }
+  return acc;
+}
+
 constexpr int kPdfMaxBins = 512;
 constexpr int kMergeMax = 1024;  // P + n_fine, power-of-two padded
 
@@ -435,9 +460,7 @@ __device__ void sample_pdf_wave(const float* __restrict__ bins, const float* __r
   for (int i = lane; i < nb + 1; i += 64) s_bins[i] = bins[i];
   __builtin_amdgcn_wave_barrier();
   __syncthreads();
-  float sum = 0.0f;
-  if (lane == 0) sum = torch_row_sum(s_w, nb);
-  sum = __shfl(sum, 0, 64);
+  const float sum = torch_row_sum_wave(s_w, nb, lane);
   // cdf = [0, cumsum(pdf)] with double accumulation
   const int S = (nb + 63) / 64;
   double local = 0.0;
@@ -496,6 +519,69 @@ __global__ void __launch_bounds__(64) sample_pdf_kernel(const float* __restrict_
                   out + ray * N, s_w, s_cdf, s_bins, threadIdx.x);
 }
 
+// Ascending bitonic sort of 64 * EPL floats held EPL per lane (element e = EPL * lane + r): partners at distance
+// j < EPL inside the lane, else across lanes (lane ^ j / EPL) through shuffles; the compare-exchange of the LDS version
+template <int EPL>
+__device__ __forceinline__ void wave_bitonic(float (&v)[EPL], int lane) {
+  constexpr int N = 64 * EPL;
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j < EPL) {
+#pragma unroll
+        for (int r = 0; r < EPL; ++r) {
+          const int rp = r ^ j;
+          if (rp > r) {
+            const bool up = ((EPL * lane + r) & k) == 0;
+            const float a = v[r], b = v[rp];
+            if ((a > b) == up) {
+              v[r] = b;
+              v[rp] = a;
+            }
+          }
+        }
+      } else {
+        const int lj = j / EPL;
+        const bool lower = (lane & lj) == 0;
+#pragma unroll
+        for (int r = 0; r < EPL; ++r) {
+          const float o = __shfl_xor(v[r], lj, 64);
+          const bool up = ((EPL * lane + r) & k) == 0;
+          // the pair (lower, upper) = (v[r] here, o) or (o, v[r]); swap iff (lower > upper) == up
+          const float lo_v = lower ? v[r] : o, hi_v = lower ? o : v[r];
+          const bool sw = (lo_v > hi_v) == up;
+          v[r] = sw ? o : v[r];
+        }
+      }
+    }
+  }
+}
+// sort row[0..n) in LDS (n <= 512) with the register bitonic of the smallest lane width that holds it
+template <int EPL>
+__device__ __forceinline__ void sort_lds_row_t(float* row, int n, int lane) {
+  float v[EPL];
+#pragma unroll
+  for (int r = 0; r < EPL; ++r) {
+    const int e = EPL * lane + r;
+    v[r] = e < n ? row[e] : __builtin_inff();
+  }
+  wave_bitonic<EPL>(v, lane);
+#pragma unroll
+  for (int r = 0; r < EPL; ++r) {
+    const int e = EPL * lane + r;
+    if (e < n) row[e] = v[r];
+  }
+}
+__device__ __forceinline__ void sort_lds_row(float* row, int n, int lane) {
+  __syncthreads();
+  if (n <= 64) sort_lds_row_t<1>(row, n, lane);
+  else if (n <= 128) sort_lds_row_t<2>(row, n, lane);
+  else if (n <= 256) sort_lds_row_t<4>(row, n, lane);
+  else sort_lds_row_t<8>(row, n, lane);
+  __syncthreads();
+}
+
 // RayPointRefiner: mids = lerp(z[1:], z[:-1], 0.5) = z[:-1] - (z[:-1] - z[1:]) * 0.5 (aten lerp, w >= 0.5
 // branch); samples from w[1:-1]; cat + sort (bitonic, LDS) .
 __global__ void __launch_bounds__(64) refine_kernel(const float* __restrict__ z, const float* __restrict__ w, int64_t R,
@@ -521,11 +607,48 @@ __global__ void __launch_bounds__(64) refine_kernel(const float* __restrict__ z,
   const int off = add_input ? P : 0;
   sample_pdf_wave(s_mid, w + ray * P + 1, P - 2, NF, det, u ? u + ray * NF : nullptr, seed, offset, ray, s_all + off,
                   s_w, s_cdf, s_bins, lane);
+  if (NF <= 64 * 8 && P <= 64 * 8) {
+    // the fine samples (and the coarse depths) sorted in registers, then merged by rank: values only, so any correct
+    // sort of the union gives torch.sort's output bit for bit
+    float* s_fine = s_all + off;
+    float* s_coarse = s_mid;  // free once sample_pdf_wave copied the bins
+    if (add_input)
+      for (int i = lane; i < P; i += 64) s_coarse[i] = zr[i];
+    __syncthreads();
+    sort_lds_row(s_fine, NF, lane);
+    if (add_input) sort_lds_row(s_coarse, P, lane);
+    __syncthreads();
+    float* orow = out + ray * total;
+    if (!add_input) {
+      for (int i = lane; i < NF; i += 64) orow[i] = s_fine[i];
+      return;
+    }
+    // merge: coarse i goes to i + #{fine < a}, fine j to j + #{coarse <= b} (ties: coarse first)
+    for (int i = lane; i < P; i += 64) {
+      const float a = s_coarse[i];
+      int lo = 0, hi = NF;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_fine[mid] < a) lo = mid + 1; else hi = mid;
+      }
+      orow[i + lo] = a;
+    }
+    for (int j = lane; j < NF; j += 64) {
+      const float b = s_fine[j];
+      int lo = 0, hi = P;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_coarse[mid] <= b) lo = mid + 1; else hi = mid;
+      }
+      orow[j + lo] = b;
+    }
+    return;
+  }
   if (add_input)
     for (int i = lane; i < P; i += 64) s_all[i] = zr[i];
   for (int i = total + lane; i < npow; i += 64) s_all[i] = __builtin_inff();
   __syncthreads();
-  // bitonic sort ascending
+  // bitonic sort ascending (sizes past the register sort)
   for (int k = 2; k <= npow; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       for (int i = lane; i < npow; i += 64) {

@@ -69,6 +69,11 @@ def main(R=4096, P=192, reps=10):
                 e.record()
                 times[k].append((s, e))
         torch.cuda.synchronize()
+        # digest of the weight gradients of one more backward: A/B variants that must be bitwise equal compare it
+        bwd()
+        torch.cuda.synchronize()
+        import hashlib
+        res[f"{prec}_grad_digest"] = hashlib.sha1(b"".join(g.cpu().numpy().tobytes() for g in grads)).hexdigest()[:16]
         flop = 2.0 * 589_952 * N
         for k, evs in times.items():
             ms = sorted(a.elapsed_time(b) for a, b in evs)

@@ -1800,6 +1800,14 @@ constexpr int DW_RPI = 64 / DW_CPR;         // rows per DMA wave-instruction
 #define YANERF_DW_PF 0
 #endif
 constexpr bool DW_PF = YANERF_DW_PF;  // fp32 dW: prefetch the next stage's fragments during the current MFMAs
+#ifndef YANERF_DW_STAGGER
+#define YANERF_DW_STAGGER 1
+#endif
+constexpr int DW_STAGGER = YANERF_DW_STAGGER;
+#ifndef YANERF_DW_ORDER
+#define YANERF_DW_ORDER 1
+#endif
+constexpr bool DW_ORDER = YANERF_DW_ORDER;  // fp32 dW: row-fragment-outer MFMA order (early first MFMA)  // fp32 dW: SIMD partners half a stage apart (2: + setprio 1 for 4-7)
 #ifndef YANERF_DW_STAGES
 #define YANERF_DW_STAGES (YANERF_DW_CPR == 4 ? 4 : 2)
 #endif
@@ -1950,6 +1958,106 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
         }
       }
     }
+  } else if constexpr (DW_STAGGER && sizeof(T) == 4 && KBS == 1) {
+    // Staggered SIMD partners (waves w and w + 4 share a SIMD). Both read stage st's fragments right after its
+    // barrier; waves 0-3 multiply k-steps 0..3 of stage st, waves 4-7 first finish k-steps 2..3 of stage st-1 from
+    // the registers they kept, then k-steps 0..1 of stage st. So while one partner waits on its LDS reads after the
+    // barrier the other has MFMAs ready. Every accumulator still sees its points in the same order (stage by stage,
+    // k-step by k-step): results are bitwise those of the unstaggered loop. LDS buffer lifetimes are unchanged (a
+    // stage's fragments are read in the segment after its barrier).
+    const bool late = wave >= 4;
+    if constexpr (DW_STAGGER == 2) {
+      if (late) __builtin_amdgcn_s_setprio(1);
+    }
+    f4 a[2][4], b[2][KTW];
+    auto read_frags = [&](const char* buf, f4 (&fa)[4], f4 (&fb)[KTW]) {
+#pragma unroll
+      for (int q = 0; q < KTW; ++q) {
+        const int row = BN + (wk * KTW + q) * 16 + li;
+        fb[q] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, g) << 4));
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int row = wn * 64 + 16 * nt + li;
+        fa[nt] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, g) << 4));
+      }
+    };
+    auto half = [&](const f4 (&fa)[4], const f4 (&fb)[KTW], int ks0) {
+#pragma unroll
+      for (int ks = ks0; ks < ks0 + 2; ++ks)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int q = 0; q < KTW; ++q)
+            acc[nt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[nt][ks], fb[q][ks], acc[nt][q], 0, 0, 0);
+    };
+#pragma unroll
+    for (int i = 0; i < RSTG - 1; ++i)
+      if (st_lo + i < st_hi) issue(st_lo + i);
+    auto begin_stage = [&](int64_t sc) {
+      const int64_t ahead = st_hi - 1 - sc;
+      static_assert(RSTG >= 2 && RSTG <= 5, "wait ladder below");
+      if (ahead >= RSTG - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (RSTG - 2)) : "memory");
+      else if (RSTG == 5 && ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * 2) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (sc + RSTG - 1 < st_hi) issue(sc + RSTG - 1);
+      return (const char*)(smem + (int)(sc % RSTG) * RSB);
+    };
+    // Separate straight-line loops per role (no branch between a stage's fragment reads and its MFMAs, so the
+    // compiler's lgkmcnt wait lands right before the first MFMA that uses the new fragments).
+    if (late && mma_wave) {
+      if (st_lo < st_hi) {
+        const char* buf = begin_stage(st_lo);
+        read_frags(buf, a[0], b[0]);
+        half(a[0], b[0], 0);
+        if (do_bias) bias_rows(buf);
+      }
+      // two stages per trip so the fragment sets alternate without register copies
+      for (int64_t st = st_lo + 1; st < st_hi; st += 2) {
+#pragma unroll
+        for (int h = 1; h >= 0; --h) {
+          const int64_t sc = st + (1 - h);
+          if (sc < st_hi) {
+            const char* buf = begin_stage(sc);
+            read_frags(buf, a[h], b[h]);
+            half(a[h ^ 1], b[h ^ 1], 2);
+            half(a[h], b[h], 0);
+            if (do_bias) bias_rows(buf);
+          }
+        }
+      }
+      if (st_hi > st_lo) {
+        if (((st_hi - 1 - st_lo) & 1) == 0) half(a[0], b[0], 2);
+        else half(a[1], b[1], 2);
+      }
+    } else {
+      for (int64_t sc = st_lo; sc < st_hi; ++sc) {
+        const char* buf = begin_stage(sc);
+        if (mma_wave) {
+          read_frags(buf, a[0], b[0]);
+          if constexpr (DW_ORDER) {
+            // row-fragment-outer: the first MFMAs need the column fragments and one row fragment
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+              for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+                for (int q = 0; q < KTW; ++q)
+                  acc[nt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][nt][ks], b[0][q][ks], acc[nt][q], 0, 0, 0);
+          } else {
+            half(a[0], b[0], 0);
+            half(a[0], b[0], 2);
+          }
+        }
+        if (do_bias) bias_rows(buf);
+      }
+    }
+    if constexpr (DW_STAGGER == 2) {
+      if (late) __builtin_amdgcn_s_setprio(0);
+    }
   } else {
 #pragma unroll
   for (int i = 0; i < RSTG - 1; ++i)
@@ -1963,12 +2071,33 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (st + RSTG - 1 < st_hi) issue(st + RSTG - 1);
+    if (!(YANERF_ABLATE & 1024)) __builtin_amdgcn_s_barrier();
+    if (!(YANERF_ABLATE & 512) && st + RSTG - 1 < st_hi) issue(st + RSTG - 1);
     const char* buf = smem + (int)(st % RSTG) * RSB;
 #pragma unroll
     for (int kb = 0; kb < KBS; ++kb)
-    if (mma_wave) {
+    if (DW_ORDER && sizeof(T) == 4 && mma_wave) {
+      // column fragments first, then one row fragment per 4 x KTW MFMA group: the first MFMAs wait for KTW + 1 of the
+      // KTW + 4 reads, not all of them (same per-accumulator k order, bitwise equal)
+      f4 a[4], b[KTW];
+#pragma unroll
+      for (int q = 0; q < KTW; ++q) {
+        const int row = BN + (wk * KTW + q) * 16 + li;
+        b[q] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, kb * 4 + g) << 4));
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int row = wn * 64 + 16 * nt + li;
+        a[nt] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, kb * 4 + g) << 4));
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+          for (int q = 0; q < KTW; ++q)
+            acc[nt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[nt][ks], b[q][ks], acc[nt][q], 0, 0, 0);
+    } else if (mma_wave) {
       f4 a[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {

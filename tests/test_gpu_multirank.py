@@ -154,13 +154,13 @@ def _trainer_worker(rank, world, port, q):
     cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml"))
     tr = NeRFTrainer(cfg.pipeline, precision="fp32", device="cuda:0", n_rays=256, runner_cfg=cfg.runner, seed=42)
     local = []
-    orig = parallel.allreduce_mean_
+    orig = parallel.allreduce_sum_async
 
-    def spy(flat):
-        local.append(flat.detach().cpu().clone())
-        return orig(flat)
+    def spy(bucket):  # the exchange's buckets (coarse slice, then fine slice) before the reduction
+        local.append(bucket.detach().cpu().clone())
+        return orig(bucket)
 
-    parallel.allreduce_mean_ = spy
+    parallel.allreduce_sum_async = spy
     g = torch.Generator().manual_seed(100 + rank)
     img = torch.rand(1, 800, 800, 3, generator=g).to("cuda:0")
     out = []
@@ -168,9 +168,10 @@ def _trainer_worker(rank, world, port, q):
         pose = torch.from_numpy(synthetic_pose(20.0 * k + 90.0 * rank, -30.0, 4.0)).float()[None].to("cuda:0")
         tr.step(pose, torch.tensor([1111.111], device="cuda:0"), img)
         torch.cuda.synchronize()
-        out.append(dict(local=local[-1], reduced=tr.flat.grad.detach().cpu().clone(),
+        assert len(local) == 2 * (k + 1)  # two buckets per step, one per model, in flat-buffer order
+        out.append(dict(local=torch.cat(local[-2:]), reduced=tr.flat.grad.detach().cpu().clone(),
                         params=tr.flat.data.detach().cpu().clone(), xys=tr.xys.detach().cpu().clone(), lr=tr.lr))
-    parallel.allreduce_mean_ = orig
+    parallel.allreduce_sum_async = orig
     q.put(_by_value((rank, out)))
     parallel.barrier()
     torch.distributed.destroy_process_group()
@@ -180,7 +181,8 @@ def test_trainer_gradient_exchange_two_ranks():
     """configs[2]'s exchange on the fused path (scripts/run.py:162-166 DDP semantics): per step, the exchanged gradient
     is the mean of the ranks' local gradients (bit for bit), the parameters stay identical on every rank, the ranks
     sample different pixels (Philox keyed by seed + rank, run.py:70-71), and the learning rate is the linearly scaled
-    schedule (run.py:152-156)."""
+    schedule (run.py:152-156). The exchange runs as two buckets (coarse model, then fine model), the coarse one
+    overlapped with the fine MLP's backward."""
     from yanerf_amd.lr_schedule import lr_at
     from yanerf_amd.utils.config import Config
     import yanerf_boot

@@ -31,10 +31,17 @@ def _worker(rank, world, port, q):
     parallel.broadcast_(fp.data)
     fp.grad.copy_(torch.arange(fp.numel, dtype=torch.float32) * (rank + 1))
     parallel.allreduce_mean_(fp.grad)
+    # the trainer's bucketed exchange: two async sums on slices of one flat buffer, then the mean
+    b = torch.arange(12, dtype=torch.float32) * (rank + 1)
+    h0 = parallel.allreduce_sum_async(b[:5])
+    h1 = parallel.allreduce_sum_async(b[5:])
+    parallel.finish_allreduce(h0)
+    parallel.finish_allreduce(h1)
+    b.div_(world)
     m = parallel.allgather_cat(torch.tensor([float(rank)]))
     mx = parallel.max_over_ranks(float(rank) + 0.5)
     shards = [list(parallel.shard_range(10, k, world)) for k in range(world)]
-    q.put(_by_value((rank, fp.data.clone(), lin[0].grad.clone(), m, mx, shards)))
+    q.put(_by_value((rank, fp.data.clone(), lin[0].grad.clone(), m, mx, shards, b)))
     parallel.barrier()
     torch.distributed.destroy_process_group()
 
@@ -50,7 +57,8 @@ def test_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, d0, g0, m0, x0, s0), (_, d1, g1, m1, x1, s1) = res
+    (_, d0, g0, m0, x0, s0, b0), (_, d1, g1, m1, x1, s1, b1) = res
+    assert torch.equal(b0, torch.arange(12, dtype=torch.float32) * 1.5) and torch.equal(b0, b1)
     assert torch.equal(d0, d1)  # broadcast from rank 0
     expect = torch.arange(15, dtype=torch.float32).view(5, 3) * 1.5  # mean of x1 and x2
     assert torch.allclose(g0, expect) and torch.allclose(g1, expect)

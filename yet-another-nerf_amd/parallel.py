@@ -57,6 +57,20 @@ def allreduce_mean_(flat: torch.Tensor) -> torch.Tensor:
     return flat
 
 
+def allreduce_sum_async(t: torch.Tensor):
+    """Start a sum all-reduce of `t` in place and return its handle (None without a process group). Under RCCL the
+    collective runs on the process group's own stream after the work already queued on the current stream, so
+    kernels queued afterwards overlap it; `finish_allreduce` makes the current stream wait for it."""
+    if not is_dist():
+        return None
+    return dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
+
+
+def finish_allreduce(handle) -> None:
+    if handle is not None:
+        handle.wait()
+
+
 def broadcast_(flat: torch.Tensor, src: int = 0) -> torch.Tensor:
     """Make every rank start from rank `src`'s parameters (DDP does this at wrap time)."""
     if is_dist():

@@ -93,6 +93,7 @@ class NeRFTrainer:
         self.specs = [m.spec() for m in self.models]
         self.params: List[List[torch.nn.Parameter]] = [m.hip_params() for m in self.models]
         self.flat = parallel.FlatParams(self.params[0] + self.params[1])
+        self.n_coarse = sum(p.numel() for p in self.params[0])  # the coarse model's slice of the flat buffers
         parallel.broadcast_(self.flat.data)
         self.world, self.rank = parallel.world_rank()
         self.rng = ops.philox_stream(int(seed) + self.rank)
@@ -282,14 +283,26 @@ class NeRFTrainer:
                                                      None, _p(noise), _p(ps.g_feats), None, None, R, P, C,
                                                      _p(ps.g_sigma), _p(ps.g_rgb), st), "yanerf_composite_backward")
             out["sq_coarse" if k == 0 else "sq_fine"] = ps.sq
-            if k == 0 and self.overlap == "early" and not self.kernel_probes:
+            if k == 0 and self.overlap == "early" and not self.kernel_probes and self.world == 1:
                 # the coarse pass's loss and gradients are complete here and nothing of the fine pass depends on them:
                 # its MLP backward (dX: MFMA-bound, dW: bandwidth-bound) runs on the side stream beside the refinement
                 # and the fine forward (MFMA-bound) instead of after it
                 self.side.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(self.side):
                     self._mlp_backward(0, ctypes.c_void_p(self.side.cuda_stream), self.side)
-        if self.kernel_probes:
+        if self.world > 1 and not self.kernel_probes:
+            # Under data parallelism the gradient exchange is split in two buckets, one per model, overlapped with
+            # the backward: the coarse MLP's backward runs first, its 2.4 MB all-reduce starts on the
+            # collective stream and runs while the fine MLP's backward (the longer one) occupies the GPU; only the
+            # fine bucket's all-reduce is exposed before Adam. Per element the result is the same sum over ranks.
+            self._mlp_backward(0, st)
+            h = parallel.allreduce_sum_async(self.flat.grad[:self.n_coarse])
+            self._mlp_backward(1, st)
+            h2 = parallel.allreduce_sum_async(self.flat.grad[self.n_coarse:])
+            parallel.finish_allreduce(h)
+            parallel.finish_allreduce(h2)
+            self.flat.grad.div_(self.world)
+        elif self.kernel_probes:
             # timing probe mode (bench.py's per-kernel roofline): every MLP backward kernel alone on the stream, in the
             # order dX, dW, slab reduce; the result is identical to the other schedules
             for k in (1, 0):
@@ -317,7 +330,8 @@ class NeRFTrainer:
                 self._mlp_backward(0, ctypes.c_void_p(self.side.cuda_stream), self.side)
             self._mlp_backward(1, st)
             torch.cuda.current_stream().wait_stream(self.side)
-        parallel.allreduce_mean_(self.flat.grad)
+        if self.world == 1 or self.kernel_probes:
+            parallel.allreduce_mean_(self.flat.grad)
         self.lr = self.current_lr()  # the reference schedules before the step (apis.py:66-68)
         self.step_count += 1
         _C.check(L.yanerf_adam(_p(self.flat.data), _p(self.flat.grad), _p(self.exp_avg), _p(self.exp_avg_sq),

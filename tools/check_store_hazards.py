@@ -9,7 +9,8 @@ stores whose soffset is not a register; on the MI355X the unguarded form lost st
 import re
 import sys
 
-STORE = re.compile(r"(buffer|global)_store_dwordx(3|4) v\[(\d+):(\d+)\]")
+# buffer stores name the data VGPRs first; global stores name the 64-bit address first, then the data
+STORE = re.compile(r"(?:buffer_store_dwordx(?:3|4) |global_store_dwordx(?:3|4) v\[\d+:\d+\], )v\[(\d+):(\d+)\]")
 WRITE = re.compile(r"(v_\S+|ds_read\S*|global_load\S*|buffer_load\S*)\s+v\[?(\d+)(?::(\d+))?")
 
 
@@ -22,7 +23,7 @@ def scan(path):
         if not m:
             continue
         n_stores += 1
-        a, b = int(m.group(3)), int(m.group(4))
+        a, b = int(m.group(1)), int(m.group(2))
         if i + 1 < len(lines):
             nxt = lines[i + 1]
             w = WRITE.match(nxt)

@@ -8,13 +8,13 @@
 
 A step = one rank's training step on one synthetic 800x800 image (4096 rays, 64 + (64+128) points per ray):
 raygen -> coarse MLP -> composite -> refine -> fine MLP -> composite -> loss -> backward (both MLPs) ->
-RCCL gradient all-reduce -> Adam. Inputs (target image, poses) are resident in HBM before timing; weights are
+RCCL gradient all-reduce (two buckets, the coarse one overlapped with the fine MLP backward) -> Adam. Inputs (target image, poses) are resident in HBM before timing; weights are
 random-init of the Lego architecture; targets are synthetic (no dataset in this environment). Weak scaling:
 every rank runs its own 4096-ray step, value = total rays of all ranks / max-over-ranks time.
 
-Rank 0 prints ONE JSON line (contract in the task statement), with `roofline` for the dominant kernel
-(fine-pass fused MLP forward, timed with HIP events on the launch stream) and `cpu_baseline` (the CPU oracle's
-training step on a bounded sample, rank 0 at N=1 only).
+Rank 0 prints ONE JSON line (contract in the task statement), with `roofline` for the dominant kernel by time
+(the fine pass's three MLP kernels, each timed alone with HIP events on its launch stream; `roofline_kernels` has all
+three) and `cpu_baseline` (the CPU oracle's training step on a bounded sample, rank 0 at N=1 only).
 """
 from __future__ import annotations
 
@@ -266,6 +266,32 @@ def extras(pcfg, cfg, dev, poses, focal, image, precision, others=()):
         "step_mfma_frac": round(train_flops_per_ray(Pc4, Pf4) * R4 / dt / 1e12 / PEAK_TFLOPS["bf16"], 4),
         "fine_fwd_ms": round(f4ms, 4), "fine_fwd_mfma_frac": round(fwd4 / (f4ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"], 4)}
     del tr
+    # BASELINE configs[3] on one GPU: the Fern config (504 x 378, 1024 rays per step) at BASELINE's 64 + 128 samples,
+    # LLFF-style per-image depth bounds (a [1, 2] tensor, averaged as ray_sampler.py:280-283 does), synthetic target.
+    # Reference CPU path on 8 cores: 341 rays/s
+    fcfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/fern.yml")).pipeline
+    fcfg.renderer.n_pts_per_ray_fine_training = 128
+    fcfg.renderer.n_pts_per_ray_fine_evaluation = 128
+    fimg = torch.rand(1, 378, 504, 3, device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+    ffocal = torch.tensor([407.56], device=dev)
+    bounds = torch.tensor([[1.3, 5.9]])  # host tensor (LLFF's bounds come from the loader on the host): no device sync
+    out["fern_64_128_train"] = {"config": "BASELINE configs[3] at 1 GPU: Fern 504x378, 64 + 128, 1024 rays, "
+                                          "per-image bounds", "reference_cpu_rays_per_s": 341.0}
+    for p in ("fp32", "bf16"):
+        tr = NeRFTrainer(fcfg, precision=p, device=dev)
+        for i in range(3):
+            tr.step(poses[i:i + 1], ffocal, fimg, near=bounds[:, :1], far=bounds[:, 1:])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        nst = 20
+        for i in range(nst):
+            tr.step(poses[(3 + i) % len(poses)][None], ffocal, fimg, near=bounds[:, :1], far=bounds[:, 1:])
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / nst
+        out["fern_64_128_train"][p] = {
+            "rays_per_s": round(tr.R / dt, 1), "ms_per_step": round(1e3 * dt, 3),
+            "step_mfma_frac": round(train_flops_per_ray(tr.Pc, tr.Pf) * tr.R / dt / 1e12 / PEAK_TFLOPS[p], 4)}
+        del tr
     return out
 
 

@@ -48,6 +48,16 @@ def main():
     gmax_w = max(grid_w.values())
     fk = [v for d, v in fetch.items() if grid_f[d] == gmax_f]
     wk = [v for d, v in write.items() if grid_w[d] == gmax_w]
+    # the fp32 / x3 dW launches of both passes have the same grid (same tiles x point splits): the fine pass reads ~3x
+    # the coarse pass's bytes, so a bimodal set keeps its upper mode (values above the geometric mean of the extremes)
+    def upper_mode(v):
+        lo, hi = min(v), max(v)
+        if lo > 0 and hi / lo > 1.5:
+            cut = (lo * hi) ** 0.5
+            return [x for x in v if x >= cut]
+        return v
+    fk = upper_mode(fk)
+    wk = upper_mode(wk)
     fetch_kb = sum(fk) / len(fk)
     write_kb = sum(wk) / len(wk)
     res = {

@@ -123,13 +123,16 @@ class NeRFTrainer:
         self.passes = [_Pass(self.specs[0], R, self.Pc, self.dev), _Pass(self.specs[1], R, self.Pf, self.dev)]
         # one backward workspace per pass: the coarse MLP backward runs on a side stream, overlapping the fine pass
         self.ws = [torch.empty(p.ws_bytes, dtype=torch.uint8, device=self.dev) for p in self.passes]
-        # measured (tools/ab_overlap.py, step ms serial -> overlapped): fp32 31.45 -> 31.22, bf16 5.53 -> 5.44,
-        # fp32x3 20.17 -> 20.36 (its dW holds 144 KB of LDS per workgroup, so the two backwards only contend): off there
+        # measured (tools/ab_overlap.py, step ms serial -> overlapped): bf16 3.741 -> 3.677 (round 2), fp32 30.82 ->
+        # 30.48, fp32x3 20.17 -> 20.36 (its dW holds 144 KB of LDS per workgroup, so the two backwards only contend).
+        # Default: on for bf16 only. In fp32 (the parity mode and the bench headline) every kernel of the step then
+        # runs alone on the GPU, so the per-kernel timings in a rocprofv3 trace of the benched steps are the kernels'
+        # own (the roofline kernel, the fine dW, is not stretched by the coarse backward beside it) at a 1 % cost.
         # overlap: False = serial, True / "both" = the whole coarse backward on the side stream beside the fine one,
         # "split" = the coarse input-side walk (dX) first on the main stream, then its weight gradients (dW, a
         # byte-bound kernel) on the side stream beside the fine dX (an MFMA-bound kernel)
         if overlap is None:
-            overlap = precision != "fp32x3"
+            overlap = precision == "bf16"
         self.overlap = "both" if overlap is True else overlap
         self.side = torch.cuda.Stream(device=self.dev) if overlap else None
         self.grad_ptrs = [_C.ptr_array([p.grad.data_ptr() for p in ps]) for ps in self.params]

@@ -50,6 +50,8 @@ def run(data_dir: Path, precision: str, steps: int, dev, n_rays=4096, log=None, 
             pose, focal, img, _, _ = train.item(i)
             tr.step(pose, focal, img)
             it += 1
+            if log and it % 500 == 0:  # progress (a long GPU run must keep writing)
+                print(f"step {it}/{steps} {time.perf_counter() - t0:.1f} s", file=log, flush=True)
         epoch += 1
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0

@@ -1790,8 +1790,11 @@ template <> __device__ __forceinline__ float hsum16<bf16_t>(f4 v) {
 // c ^ (2 * ((r >> 3) & 1)), conflict-free for the 16x16 fragment reads) goes on the SOURCE chunk. One raw barrier
 // per stage: after it every wave's DMA for this stage has landed (each wave waited for its own with a counted
 // vmcnt) and every wave is done reading the buffer the next DMA overwrites.
+// fp32 dW: two K-blocks (32 points) per stage in a 3-deep ring of 48 KB stages: half the stage barriers of one
+// K-block per stage (round 2, with the two-K-block stagger below: 7.98 -> 7.86 ms). The x3 dW keeps its own 64-byte
+// rows (dw_swz4).
 #ifndef YANERF_DW_CPR
-#define YANERF_DW_CPR 4
+#define YANERF_DW_CPR 8
 #endif
 constexpr int DW_CPR = YANERF_DW_CPR;      // 16-byte chunks per staged row (4: one K-block, 8: two)
 constexpr int DW_RB = 16 * DW_CPR;          // staged row bytes
@@ -1812,11 +1815,12 @@ constexpr bool DW_ORDER = YANERF_DW_ORDER;  // fp32 dW: row-fragment-outer MFMA 
 #define YANERF_DW_STAGES (YANERF_DW_CPR == 4 ? 4 : 2)
 #endif
 constexpr int DW_STAGES = YANERF_DW_STAGES, DW_STAGE_BYTES = 512 * DW_RB;
-// fp32 ring: a stage holds at most 256 + 128 rows (dw_bkmax 128), 4 stages = 96 KB. (3 stages = 72 KB let two
-// workgroups share a CU -- 16 waves, 4 per SIMD, at the tile's 116 VGPRs -- and measured slower: fp32 dW 8.15 ->
-// 8.33 ms; the fp32 dW's idle MFMA cycles are not stage-barrier bubbles another workgroup could fill.)
+// fp32 ring: a stage holds at most 256 + 128 rows (dw_bkmax 128): 3 stages of 48 KB (two K-blocks per row) = 144 KB,
+// or with one K-block per row 4 stages of 24 KB = 96 KB. (With one K-block, 3 stages = 72 KB let two workgroups share
+// a CU -- 16 waves, 4 per SIMD, at the tile's 116 VGPRs -- and measured slower: fp32 dW 8.15 -> 8.33 ms; the fp32
+// dW's idle MFMA cycles are not stage-barrier bubbles another workgroup could fill.)
 #ifndef YANERF_DW32_STAGES
-#define YANERF_DW32_STAGES 4
+#define YANERF_DW32_STAGES (YANERF_DW_CPR == 4 ? 4 : 3)
 #endif
 template <typename T> struct DwRing {
   static constexpr int STAGES = DW_STAGES, STAGE_BYTES = DW_STAGE_BYTES;
@@ -1831,9 +1835,8 @@ static int64_t dw_stage_pts(int prec) {
   if (prec == YANERF_PREC_BF16 && YANERF_BF16_PM) return YANERF_PM_SPTS;
   return (prec == YANERF_PREC_F32 ? Cfg<float>::KB : Cfg<bf16_t>::KB) * (DW_CPR / 4);
 }
-__device__ __forceinline__ int dw_swz(int row, int c) {
-  return DW_CPR == 4 ? (c ^ (((row >> 3) & 1) << 1)) : (c ^ ((row >> 1) & 7));
-}
+__device__ __forceinline__ int dw_swz4(int row, int c) { return c ^ (((row >> 3) & 1) << 1); }  // 64-byte rows
+__device__ __forceinline__ int dw_swz(int row, int c) { return DW_CPR == 4 ? dw_swz4(row, c) : (c ^ ((row >> 1) & 7)); }
 
 template <typename T, int BN, int BK>
 __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, int64_t Npad, float* __restrict__ slab,
@@ -1956,6 +1959,86 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
           mma(a[h], b[h]);
           if (do_bias) bias_rows(smem + (int)(sc % RSTG) * RSB);
         }
+      }
+    }
+  } else if constexpr (DW_STAGGER && sizeof(T) == 4 && KBS == 2) {
+    // Two K-blocks per stage (YANERF_DW_CPR = 8: half the stage barriers), staggered by one K-block: waves 4-7 multiply
+    // the previous stage's second K-block (kept in registers) and then this stage's first, waves 0-3 both K-blocks of
+    // this stage. Per accumulator the points still arrive in order: bitwise equal to the other loops.
+    const bool late = wave >= 4;
+    f4 a0[4], b0[KTW], a1[2][4], b1[2][KTW];
+    auto rf = [&](const char* buf, int kb, f4 (&fa)[4], f4 (&fb)[KTW]) {
+#pragma unroll
+      for (int q = 0; q < KTW; ++q) {
+        const int row = BN + (wk * KTW + q) * 16 + li;
+        fb[q] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, kb * 4 + g) << 4));
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int row = wn * 64 + 16 * nt + li;
+        fa[nt] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, kb * 4 + g) << 4));
+      }
+    };
+    auto kblock = [&](const f4 (&fa)[4], const f4 (&fb)[KTW]) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+          for (int q = 0; q < KTW; ++q)
+            acc[nt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[nt][ks], fb[q][ks], acc[nt][q], 0, 0, 0);
+    };
+#pragma unroll
+    for (int i = 0; i < RSTG - 1; ++i)
+      if (st_lo + i < st_hi) issue(st_lo + i);
+    auto begin_stage = [&](int64_t sc) {
+      const int64_t ahead = st_hi - 1 - sc;
+      static_assert(RSTG >= 2 && RSTG <= 5, "wait ladder below");
+      if (ahead >= RSTG - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (RSTG - 2)) : "memory");
+      else if (RSTG == 5 && ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * 2) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (sc + RSTG - 1 < st_hi) issue(sc + RSTG - 1);
+      return (const char*)(smem + (int)(sc % RSTG) * RSB);
+    };
+    if (late && mma_wave) {
+      if (st_lo < st_hi) {
+        const char* buf = begin_stage(st_lo);
+        rf(buf, 0, a0, b0);
+        rf(buf, 1, a1[0], b1[0]);
+        kblock(a0, b0);
+        if (do_bias) bias_rows(buf);
+      }
+      for (int64_t st = st_lo + 1; st < st_hi; st += 2) {
+#pragma unroll
+        for (int h = 1; h >= 0; --h) {
+          const int64_t sc = st + (1 - h);
+          if (sc < st_hi) {
+            const char* buf = begin_stage(sc);
+            rf(buf, 0, a0, b0);
+            rf(buf, 1, a1[h], b1[h]);
+            kblock(a1[h ^ 1], b1[h ^ 1]);
+            kblock(a0, b0);
+            if (do_bias) bias_rows(buf);
+          }
+        }
+      }
+      if (st_hi > st_lo) {
+        if (((st_hi - 1 - st_lo) & 1) == 0) kblock(a1[0], b1[0]);
+        else kblock(a1[1], b1[1]);
+      }
+    } else {
+      for (int64_t sc = st_lo; sc < st_hi; ++sc) {
+        const char* buf = begin_stage(sc);
+        if (mma_wave) {
+          rf(buf, 0, a0, b0);
+          rf(buf, 1, a1[0], b1[0]);
+          kblock(a0, b0);
+          kblock(a1[0], b1[0]);
+        }
+        if (do_bias) bias_rows(buf);
       }
     }
   } else if constexpr (DW_STAGGER && sizeof(T) == 4 && KBS == 1) {
@@ -2559,7 +2642,7 @@ __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S,
       else p = (const float*)J.X0;
     }
     src[i] = p + seg * 4;
-    dst[i] = row < ROWS ? row * 64 + (dw_swz(row, seg >> 1) << 4) + (seg & 1) * 8 : -1;
+    dst[i] = row < ROWS ? row * 64 + (dw_swz4(row, seg >> 1) << 4) + (seg & 1) * 8 : -1;
   }
   f4 regs[LPT];
   auto load = [&](int64_t st) {
@@ -2607,7 +2690,7 @@ __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S,
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           const int row = wn * 64 + 16 * nt + li;
-          a[pl][nt] = *(const f4*)(buf + pl * PLB + row * 64 + (dw_swz(row, g) << 4));
+          a[pl][nt] = *(const f4*)(buf + pl * PLB + row * 64 + (dw_swz4(row, g) << 4));
         }
       constexpr int QG = KTW < 4 ? KTW : 4;
 #pragma unroll
@@ -2618,7 +2701,7 @@ __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S,
 #pragma unroll
           for (int q = 0; q < QG; ++q) {
             const int row = BN + (wk * KTW + q0 + q) * 16 + li;
-            b[pl][q] = *(const f4*)(buf + pl * PLB + row * 64 + (dw_swz(row, g) << 4));
+            b[pl][q] = *(const f4*)(buf + pl * PLB + row * 64 + (dw_swz4(row, g) << 4));
           }
         constexpr int TI[6] = {2, 1, 0, 1, 0, 0}, TJ[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll

@@ -1806,11 +1806,11 @@ constexpr bool DW_PF = YANERF_DW_PF;  // fp32 dW: prefetch the next stage's frag
 #ifndef YANERF_DW_STAGGER
 #define YANERF_DW_STAGGER 1
 #endif
-constexpr int DW_STAGGER = YANERF_DW_STAGGER;
+constexpr int DW_STAGGER = YANERF_DW_STAGGER;  // fp32 dW: SIMD partners staggered (2: + setprio 1 for waves 4-7)
 #ifndef YANERF_DW_ORDER
 #define YANERF_DW_ORDER 1
 #endif
-constexpr bool DW_ORDER = YANERF_DW_ORDER;  // fp32 dW: row-fragment-outer MFMA order (early first MFMA)  // fp32 dW: SIMD partners half a stage apart (2: + setprio 1 for 4-7)
+constexpr bool DW_ORDER = YANERF_DW_ORDER;  // fp32 dW: row-fragment-outer MFMA order (early first MFMA)
 #ifndef YANERF_DW_STAGES
 #define YANERF_DW_STAGES (YANERF_DW_CPR == 4 ? 4 : 2)
 #endif
@@ -1964,7 +1964,8 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
   } else if constexpr (DW_STAGGER && sizeof(T) == 4 && KBS == 2) {
     // Two K-blocks per stage (YANERF_DW_CPR = 8: half the stage barriers), staggered by one K-block: waves 4-7 multiply
     // the previous stage's second K-block (kept in registers) and then this stage's first, waves 0-3 both K-blocks of
-    // this stage. Per accumulator the points still arrive in order: bitwise equal to the other loops.
+    // this stage. Per accumulator the points still arrive in order: bitwise equal to the unstaggered loop with the same
+    // stage size.
     const bool late = wave >= 4;
     f4 a0[4], b0[KTW], a1[2][4], b1[2][KTW];
     auto rf = [&](const char* buf, int kb, f4 (&fa)[4], f4 (&fb)[KTW]) {

@@ -1496,12 +1496,38 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   }
 }
 
+// ---- the colour layer's direction columns by rays (YANERF_DIRPE_RAY). LinearWithRepeat (nerf_mlp.py) feeds every
+// point of a ray the same direction embedding, so dW_dir[c][k] = sum_p dZc[p][c] dirPE[ray(p)][k]
+// = sum_r dirPE[r][k] (sum_{p in r} dZc[p][c]). The dX kernel sums dZc per ray over each thread-chunk of its tile
+// (dzc_chunk points, ascending), the block kernel adds a ray's chunk partials (ascending) and accumulates the products
+// over blocks of DIRB rays (ascending), the final kernel adds the blocks (ascending): deterministic, and a 128 x 27
+// product over R rays replaces a 128 x 64 dW tile over every point. Used when P >= dzc_chunk (a ray then touches at
+// most two partials per chunk slot).
+#ifndef YANERF_DIRPE_RAY
+#define YANERF_DIRPE_RAY 1
+#endif
+template <typename T> __host__ __device__ constexpr int dzc_chunk() { return Cfg<T>::M / (Cfg<T>::DXWAVES * 64 / HC); }
+constexpr int DIRB = 16;  // rays per block of the dirPE product
+template <typename T> __device__ __forceinline__ float lds_val(const typename Cfg<T>::lds_t* act, int m, int col);
+template <> __device__ __forceinline__ float lds_val<float>(const float* act, int m, int col) {
+  return act[lds_idx<float>(m, col)];
+}
+template <> __device__ __forceinline__ float lds_val<bf16_t>(const bf16_t* act, int m, int col) {
+  return bf2f(act[lds_idx<bf16_t>(m, col)]);
+}
+template <> __device__ __forceinline__ float lds_val<x3_t>(const bf16_t* act, int m, int col) {
+  constexpr int PL = Cfg<x3_t>::M * ROW;  // exact: the three planes hold disjoint bits of the fp32 value
+  const int i = lds_idx<x3_t>(m, col);
+  return (bf2f(act[i]) + bf2f(act[PL + i])) + bf2f(act[2 * PL + i]);
+}
+
 // ============================================================================================ backward dX
 template <typename T>
 __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_bwd_dx_kernel(
     MlpLayout lay, const typename Cfg<T>::w_t* __restrict__ Wt, const float* __restrict__ Wf,
     const uint64_t* __restrict__ masks, const float* __restrict__ rgb, const float* __restrict__ g_sigma,
-    const float* __restrict__ g_rgb, int64_t N, int64_t Npad, typename Cfg<T>::st_t* __restrict__ grad) {
+    const float* __restrict__ g_rgb, int64_t N, int64_t Npad, typename Cfg<T>::st_t* __restrict__ grad, int64_t P,
+    float* __restrict__ dzc_part) {
   constexpr int M = Cfg<T>::M, WAVES = Cfg<T>::DXWAVES, MT = M / 16;
   // ReLU-mask words: the forward (Cfg::WAVES waves) wrote mask_w<T>() words per lane per layer; a dX wave whose
   // NT x MT tiles are exactly one 16-tile word of a forward wave reads that word at the same index
@@ -1647,6 +1673,24 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
   // forward's trunk loop on the shared, in-order vmcnt
   if constexpr (PM)
     save_grad_pm<T, NTHR, HC>(act, gb + PG.dzc + p0 * HC * PM_GB, g8scl + (lay.L + 1) * ntile, g8red, WAVES, tid);
+  if (dzc_part) {
+    // per-ray sums of dZc over this thread's chunk of the tile (column c), for the dirPE weight gradient by rays
+    constexpr int CH = dzc_chunk<T>();
+    static_assert(NTHR % HC == 0 && CH * (NTHR / HC) == M, "dZc chunks");
+    const int c = tid % HC, ul = tid / HC;
+    const int64_t pc0 = p0 + (int64_t)ul * CH, u = pc0 / CH;
+    // P >= CH: the chunk holds the tail of its first ray [0, nb) and at most the head of the next [nb, n)
+    const int n = (int)(N - pc0 < CH ? (N - pc0 > 0 ? N - pc0 : 0) : CH);
+    const int nb = (int)(P - pc0 % P) < n ? (int)(P - pc0 % P) : n;
+    const int m0 = ul * CH;
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < nb; ++i) s0 += lds_val<T>(act, m0 + i, c);
+#pragma unroll 8
+    for (int i = nb; i < n; ++i) s1 += lds_val<T>(act, m0 + i, c);
+    if (n > 0) dzc_part[(u * 2) * HC + c] = s0;
+    if (n > nb) dzc_part[(u * 2 + 1) * HC + c] = s1;
+  }
   lds_barrier();
   G8Max gmax;
 #pragma unroll
@@ -1749,6 +1793,7 @@ struct DwJob {
   // a_chunks = 16-byte chunks of A per point that hold data; the tile's column space is "virtual": X0's columns
   // padded to x0p (a multiple of 8), then X1's (ktot_v = x0p + x1_rows); k-tiles are laid over ktot_v
   int a_ld, a_chunks, x0_ld, x1_ld, x0p, ktot_v;
+  int w_ld;  // row stride of W: ktot, or more when trailing columns come from elsewhere (the per-ray dirPE term)
   int x0_u8, x1_u8;  // X0 / X1 stored as fp8 e4m3 (YANERF_BF16_A8: the post-ReLU sections); a k-tile is one format
   int a_u8;          // A stored as fp8 e4m3 of value / scale (YANERF_BF16_G8: dZ_l, dY, dZc; not dU)
   const float* a_scale;  // A's decode scale per 128-point tile
@@ -2825,6 +2870,75 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   }
 }
 
+// dirPE of ray r, column k: kind 0 = fp32 feature-major saved rows (ld floats apart), 1 = bf16 point-major [Npad][KDIR]
+__device__ __forceinline__ float dirpe_at(const void* dpe, int kind, int64_t ld, int64_t p, int k) {
+  if (kind == 0) return ((const float*)dpe)[(int64_t)k * ld + p];
+  return bf2f(((const bf16_t*)dpe)[p * KDIR + k]);
+}
+// One block per DIRB rays: the rays' dirPE rows and dZc sums staged in LDS, then thread (c, k-half) accumulates its
+// 16 products over the block's rays in ray order. Point indices fit 32 bits (the host checks).
+__global__ void __launch_bounds__(256) dirpe_dw_block_kernel(const float* __restrict__ part, int R, int P, int CH,
+                                                             const void* __restrict__ dpe, int kind, int64_t ld,
+                                                             int kd, float* __restrict__ blockp) {
+  __shared__ float Dl[DIRB][KDIR + 1];
+  __shared__ float Sl[DIRB][HC];
+  const int tid = threadIdx.x, r0 = blockIdx.x * DIRB;
+#pragma unroll 8
+  for (int i = tid; i < DIRB * KDIR; i += 256) {
+    const int r = i % DIRB, k = i / DIRB;
+    Dl[r][k] = (r0 + r < R && k < kd) ? dirpe_at(dpe, kind, ld, (int64_t)(r0 + r) * P, k) : 0.f;
+  }
+  {
+    const int c = tid % HC;
+#pragma unroll
+    for (int r = tid / HC; r < DIRB; r += 256 / HC) {
+      const int rr = r0 + r;
+      float sr = 0.f;
+      if (rr < R) {
+        const unsigned pa = (unsigned)rr * (unsigned)P, u0 = pa / CH, u1 = (pa + P - 1) / CH;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {  // predicated, so a ray's (<= 4 for P <= 3 CH) partials load together
+          const unsigned u = u0 + j;
+          v[j] = u <= u1 ? part[((int64_t)u * 2 + (rr - u * CH / P)) * HC + c] : 0.f;
+        }
+        sr = ((v[0] + v[1]) + v[2]) + v[3];
+        for (unsigned u = u0 + 4; u <= u1; ++u) sr += part[((int64_t)u * 2 + (rr - u * CH / P)) * HC + c];
+      }
+      Sl[r][c] = sr;
+    }
+  }
+  __syncthreads();
+  const int c = tid % HC, k0 = (tid / HC) * (KDIR / 2);
+  float acc[KDIR / 2];
+#pragma unroll
+  for (int k = 0; k < KDIR / 2; ++k) acc[k] = 0.f;
+  for (int r = 0; r < DIRB; ++r) {
+    const float sv = Sl[r][c];
+#pragma unroll
+    for (int k = 0; k < KDIR / 2; ++k) acc[k] += sv * Dl[r][k0 + k];
+  }
+  float* out = blockp + ((int64_t)blockIdx.x * HC + c) * KDIR + k0;
+#pragma unroll
+  for (int k = 0; k < KDIR / 2; k += 4) *(f4*)(out + k) = f4{acc[k], acc[k + 1], acc[k + 2], acc[k + 3]};
+}
+__global__ void __launch_bounds__(256) dirpe_dw_final_kernel(const float* __restrict__ blockp, int nblk, int kd,
+                                                             float* __restrict__ W, int w_ld, int col0) {
+  __shared__ float red[8][KDIR];
+  const int c = blockIdx.x, k = threadIdx.x % KDIR, g = threadIdx.x / KDIR;
+  float s = 0.f;
+#pragma unroll 8
+  for (int b = g; b < nblk; b += 8) s += blockp[((int64_t)b * HC + c) * KDIR + k];
+  red[g][k] = s;
+  __syncthreads();
+  if (g == 0 && k < kd) {
+    float t = red[0][k];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) t += red[i][k];
+    W[(int64_t)c * w_ld + col0 + k] = t;
+  }
+}
+
 // Sums the S split slabs in split order (deterministic): a thread owns 4 consecutive slab elements and reads them as
 // one 16-byte load per split, 8 splits' loads in flight before their adds (the slab stride is padded to a multiple of
 // 4 elements, dw_slab_pad); the sum order per element is s = 0, 1, ..., S - 1 as before.
@@ -2853,7 +2967,7 @@ __global__ void dw_reduce_kernel(DwJobs jobs, int S, const float* __restrict__ s
     const int64_t local = e - J.slab_off;
     const int kv = J.ktot + 1;
     const int n = (int)(local / kv), k = (int)(local % kv);
-    if (k < J.ktot) J.W[(int64_t)n * J.ktot + k] = vals[i];
+    if (k < J.ktot) J.W[(int64_t)n * J.w_ld + k] = vals[i];
     else J.b[n] = vals[i];
   }
 }
@@ -2950,7 +3064,7 @@ struct DwSpec {
   int gi;
 };
 template <typename F>
-static void for_each_dw_job(const MlpLayout& L, bool pm, F&& f) {
+static void for_each_dw_job(const MlpLayout& L, bool pm, F&& f, bool dir_by_ray = false) {
   const SavedRows SR = saved_rows(L.L);
   const GradRows GR = grad_rows(L.L, pm);
   for (int l = 0; l < L.L; ++l) {
@@ -2965,7 +3079,9 @@ static void for_each_dw_job(const MlpLayout& L, bool pm, F&& f) {
   const int h = 2 * L.L;
   const int64_t hl = SR.h0 + 256LL * (L.L - 1);
   f(DwSpec{GR.dyx, L.hid, 256, 0, hl, L.hid, 256, -1, 0, 0, h + 0});                      // intermediate_linear
-  f(DwSpec{GR.dzc, L.hdir, HC, 0, SR.y, L.hid, 256, SR.dpe, L.dir_dim, KDIR, h + 4});     // color_layer.0
+  if (dir_by_ray)  // the dirPE columns come from the per-ray reduction (dirpe_dw_*_kernel), not from a k-tile
+    f(DwSpec{GR.dzc, L.hdir, HC, 0, SR.y, L.hid, 256, -1, 0, 0, h + 4});
+  else f(DwSpec{GR.dzc, L.hdir, HC, 0, SR.y, L.hid, 256, SR.dpe, L.dir_dim, KDIR, h + 4});     // color_layer.0
   if (pm) f(DwSpec{GR.du, 1, 16, PM_DSIG, hl, L.hid, 256, -1, 0, 0, h + 2});             // density_layer
   else f(DwSpec{GR.dyx + 256, 1, 256, 0, hl, L.hid, 256, -1, 0, 0, h + 2});
   f(DwSpec{GR.du, L.cdim, 16, 0, SR.c, L.hdir, HC, -1, 0, 0, h + 6});                    // color_layer.2
@@ -2985,7 +3101,7 @@ static int dw_x0p(const MlpLayout& L, bool pm, const DwSpec& sp) {
 // a split's slab stride: whole 16-byte groups, so the reduce reads every split with aligned 16-byte loads
 static int64_t dw_slab_pad(int64_t e) { return (e + 3) / 4 * 4; }
 static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void* gradbuf, int64_t Npad,
-                          float* const* grads, DwJobs& D) {
+                          float* const* grads, DwJobs& D, bool dir_by_ray = false) {
   const size_t es = elem_size(prec);
   const bool pm = prec_pm(prec);
   const int64_t ld = pm ? Npad : row_ld(Npad, es);
@@ -3033,6 +3149,8 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     }
     j.x0_rows = sp.x0_rows; j.x1_rows = sp.x1_rows;
     j.ktot = sp.x0_rows + sp.x1_rows;
+    // the colour layer without its dirPE columns still writes rows of hid + dir_dim weights
+    j.w_ld = (dir_by_ray && sp.gi == 2 * L.L + 4) ? j.ktot + L.dir_dim : j.ktot;
     j.a_ld = sp.a_w; j.x0_ld = sp.x0_w; j.x1_ld = sp.x1_w;
     if (pm) j.A = (const char*)j.A + (int64_t)sp.a_col * a_es;
     j.a_chunks = (sp.a_w - sp.a_col) * a_es / 16;
@@ -3046,7 +3164,7 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     D.slab_elems += (int64_t)sp.a_rows * (j.ktot + 1);
     j.W = grads[sp.gi];
     j.b = grads[sp.gi + 1];
-  });
+  }, dir_by_ray);
   D.slab_stride = dw_slab_pad(D.slab_elems);
 }
 
@@ -3090,26 +3208,38 @@ static int launch_fwd(const MlpLayout& L, int prec, const void* packed, const fl
 
 template <typename T>
 static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const void* saved, const float* rgb,
-                      const float* gs, const float* gr, int64_t N, float* const* grads, void* ws, hipStream_t st,
-                      int phase) {
+                      const float* gs, const float* gr, int64_t R, int64_t P, float* const* grads, void* ws,
+                      hipStream_t st, int phase) {
   typedef typename Cfg<T>::st_t ST;
+  const int64_t N = R * P;
   const int64_t Npad = npad_of(prec, N);
   const typename Cfg<T>::w_t* Wt = (const typename Cfg<T>::w_t*)packed;
   const float* Wf = (const float*)((const char*)packed + L.f_base);
   ST* gradbuf = (ST*)ws;
   const int64_t grad_bytes = grad_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM);
   float* slab = (float*)((char*)ws + grad_bytes);
+  // the point splits and slab size are those of the full job set (yanerf_mlp_bwd_workspace_bytes)
+  int tiles_all = 0;
+  const int64_t slab_all = dw_slab_elems_for(L, prec, &tiles_all);
+  const int S = dw_splits(tiles_all, Npad / dw_stage_pts(prec), Cfg<T>::PM);
+  // the dirPE weight gradient by rays: per-ray dZc partials after the slabs, then the block partials
+  constexpr int CH = dzc_chunk<T>();
+  // default (1): fp32 only, where it measured -0.21 ms of 15.2 ms per Lego fine backward; bf16 and fp32x3 gained
+  // less in dW than the per-ray sums cost in dX; 2 forces it for every precision
+  const bool dir_by_ray = (YANERF_DIRPE_RAY == 2 || (YANERF_DIRPE_RAY == 1 && std::is_same<T, float>::value)) && P >= CH && L.dir_dim <= KDIR && L.hdir <= HC && Npad < (1ll << 31);
+  float* dzc_part = (float*)((char*)slab + (int64_t)S * slab_all * 4);
+  float* blockp = dzc_part + 2 * (Npad / CH) * HC;
   const uint64_t* masks = (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM));
   if (phase & 1) {
     hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::DXWAVES * 64), 0, st, L,
-                       Wt, Wf, masks, rgb, gs, gr, N, Npad, gradbuf);
+                       Wt, Wf, masks, rgb, gs, gr, N, Npad, gradbuf, P, dir_by_ray ? dzc_part : nullptr);
     YN_LAUNCH_CHECK("mlp_backward_dx");
   }
   // phase 2 = dW + reduce; 4 = the dW kernel alone, 8 = the slab reduce alone (4 then 8 == 2: for timing probes)
   const bool dw = (phase & 2) || (phase & 4), red = (phase & 2) || (phase & 8);
   if (!dw && !red) return 0;
   DwJobs D;
-  build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D);
+  build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D, dir_by_ray);
   for (int i = 0; i < D.n; ++i)  // a point-major k-tile reads one X format: mixed sections must split at a tile edge
     YN_CHECK(!D.j[i].X1 || D.j[i].x0_u8 == D.j[i].x1_u8 || D.j[i].x0p % dw_bkmax(prec) == 0,
              "mlp_backward: dW job %d mixes fp8 and bf16 columns inside a tile", i);
@@ -3126,7 +3256,7 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   for (int i = 0; i < D.n; ++i)  // the dW tile's A format follows its row tile (dw_tile_pm's A8)
     YN_CHECK(!Cfg<T>::PM || D.j[i].bn == 64 || D.j[i].a_u8 == YANERF_BF16_G8,
              "mlp_backward: dW job %d: gradient format %d does not match its %d-row tile", i, D.j[i].a_u8, D.j[i].bn);
-  const int S = dw_splits(D.total_tiles, Npad / dw_stage_pts(prec), Cfg<T>::PM);
+  YN_CHECK(D.slab_stride <= dw_slab_pad(slab_all), "mlp_backward: dW slab larger than its workspace");
   if (dw) {
     hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)(D.total_tiles * S)), dim3(DW_THREADS), 0, st, D, Npad, S,
                        slab);
@@ -3135,6 +3265,21 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   if (red) {
     hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((D.slab_elems + 1023) / 1024)), dim3(256), 0, st, D, S, slab);
     YN_LAUNCH_CHECK("mlp_backward_reduce");
+    if (dir_by_ray) {
+      const int gi = 2 * L.L + 4;  // color_layer.0 weight [hdir][hid + dir_dim]
+      const SavedRows SR = saved_rows(L.L);
+      const PmSave PS = pm_save(L.L, Npad);
+      const bool pm = Cfg<T>::PM;
+      const void* dpe = pm ? (const void*)((const char*)saved + PS.dpe)
+                           : (const void*)((const char*)saved + SR.dpe * row_ld(Npad, sizeof(ST)) * sizeof(ST));
+      const int nblk = (int)((R + DIRB - 1) / DIRB);
+      hipLaunchKernelGGL(dirpe_dw_block_kernel, dim3((unsigned)nblk), dim3(256), 0, st, dzc_part, (int)R, (int)P, CH, dpe,
+                         pm ? 1 : 0, row_ld(Npad, sizeof(ST)), L.dir_dim, blockp);
+      YN_LAUNCH_CHECK("mlp_backward_dirpe_block");
+      hipLaunchKernelGGL(dirpe_dw_final_kernel, dim3((unsigned)L.hdir), dim3(256), 0, st, blockp, nblk, L.dir_dim,
+                         grads[gi], L.hid + L.dir_dim, L.hid);
+      YN_LAUNCH_CHECK("mlp_backward_dirpe_final");
+    }
   }
   return 0;
 }
@@ -3192,7 +3337,11 @@ int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, 
   int tiles = 0;
   int64_t se = dw_slab_elems_for(L, precision, &tiles);
   int S = dw_splits(tiles, Npad / dw_stage_pts(precision), prec_pm(precision));
-  return grad_bytes + (int64_t)S * se * 4;
+  // + the per-ray dZc partials (two slots per dZc chunk) and the dirPE block partials (rays >= chunks when used)
+  const int CH = precision == YANERF_PREC_F32 ? dzc_chunk<float>()
+                 : precision == YANERF_PREC_BF16 ? dzc_chunk<bf16_t>() : dzc_chunk<x3_t>();
+  const int64_t nblk = (Npad / CH + DIRB - 1) / DIRB + 1;
+  return grad_bytes + (int64_t)S * se * 4 + (2 * (Npad / CH) * HC + nblk * HC * KDIR) * 4;
 }
 
 int yanerf_mlp_forward(const yanerf_mlp_desc* d, int precision, const void* packed, const float* origins,
@@ -3232,13 +3381,13 @@ int yanerf_mlp_backward_phase(const yanerf_mlp_desc* d, int precision, const voi
   if (R * P == 0) return 0;
   MlpLayout L = make_layout(d, precision);
   if (precision == YANERF_PREC_F32)
-    return launch_bwd<float>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R * P, grads, workspace,
+    return launch_bwd<float>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R, P, grads, workspace,
                              as_stream(stream), phase);
   if (precision == YANERF_PREC_BF16)
-    return launch_bwd<bf16_t>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R * P, grads, workspace,
+    return launch_bwd<bf16_t>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R, P, grads, workspace,
                               as_stream(stream), phase);
   if (precision == YANERF_PREC_F32X3)
-    return launch_bwd<x3_t>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R * P, grads, workspace,
+    return launch_bwd<x3_t>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R, P, grads, workspace,
                             as_stream(stream), phase);
   YN_CHECK(false, "mlp_backward: bad precision %d", precision);
 }

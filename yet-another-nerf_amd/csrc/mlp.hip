@@ -622,10 +622,29 @@ __device__ __forceinline__ void ring_fill(ARing<T, NT>& R, const typename Cfg<T>
 
 // Accumulator layout: acc[nt][mt] lane (g, li) holds features nrow0 + 16nt + 4g .. +3 of point 16mt + li. The
 // accumulators start from the bias when one is given (the reference's addmm also accumulates onto the bias).
-template <typename T, int NT, int MT>
+// fp32 forward: the saved rows of the GEMM's input (post-ReLU H of the previous layer, as the LDS tile holds it) are
+// written from the B fragments during the GEMM instead of from the accumulators in the previous epilogue
+// (YANERF_F32_GSAVE). Wave w stores K-blocks kb = w, w + 4, ... (all of the tile's points), after that K-block's MFMAs:
+// each weight wait then covers the stores of one earlier K-block rather than the whole epilogue's burst.
+#ifndef YANERF_F32_GSAVE
+#define YANERF_F32_GSAVE 1
+#endif
+#ifndef YANERF_F32_GSAVE_DX
+#define YANERF_F32_GSAVE_DX 0
+#endif
+struct RowSave {
+  float* base;    // saved row of the GEMM's feature 0 at the tile's first point
+  uint32_t voff;  // this lane's byte offset in a 16x16 row tile (4g rows + li points)
+  int ldb;        // row stride, bytes
+  int nkb;        // K-blocks to store (the H columns; a skip layer's PE columns are saved elsewhere)
+  int wave, waves;
+};
+
+template <typename T, int NT, int MT, bool RSV = false>
 __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict__ W, int64_t wplane, int ldw, int nrow0,
                                          const typename Cfg<T>::lds_t* act, int kc0, int nkb, f4 (&acc)[NT][MT],
-                                         int lane, const float* __restrict__ bias, ARing<T, NT>& R) {
+                                         int lane, const float* __restrict__ bias, ARing<T, NT>& R,
+                                         const RowSave& rs = RowSave{}) {
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
   // an opaque copy of the lane id: the per-K-block LDS fragment addresses (the row swizzle makes each one distinct)
   // and weight pointers are then recomputed at every call instead of being hoisted out of the caller's layer loop,
@@ -843,6 +862,21 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
     if constexpr (YANERF_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     mma_grid<T, NT, MT>(a, b, acc);
     if constexpr (YANERF_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    if constexpr (RSV) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (kb < rs.nkb && kb % rs.waves == rs.wave) {
+        char* rb = (char*)rs.base + (int64_t)(16 * kb) * rs.ldb;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          char* q = rb + 16 * mt * 4 + rs.voff;
+          *(float*)q = b[mt].x;
+          *(float*)(q + rs.ldb) = b[mt].y;
+          *(float*)(q + 2 * (int64_t)rs.ldb) = b[mt].z;
+          *(float*)(q + 3 * (int64_t)rs.ldb) = b[mt].w;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) a[nt] = an[nt];
   }
@@ -850,17 +884,17 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
 
 // gemm_run with a weight ring: `pre` was filled by the caller (ring_fill before the previous epilogue), else a local
 // one is filled here. (Two call paths, no pointer select, so the ring stays in registers.)
-template <typename T, int NT, int MT>
+template <typename T, int NT, int MT, bool RSV = false>
 __device__ __forceinline__ void gemm_lds(const typename Cfg<T>::w_t* __restrict__ W, int64_t wplane, int ldw, int nrow0,
                                          const typename Cfg<T>::lds_t* act, int kc0, int nkb, f4 (&acc)[NT][MT],
                                          int lane, const float* __restrict__ bias = nullptr,
-                                         ARing<T, NT>* pre = nullptr) {
+                                         ARing<T, NT>* pre = nullptr, const RowSave& rs = RowSave{}) {
   if (pre) {
-    gemm_run<T, NT, MT>(W, wplane, ldw, nrow0, act, kc0, nkb, acc, lane, bias, *pre);
+    gemm_run<T, NT, MT, RSV>(W, wplane, ldw, nrow0, act, kc0, nkb, acc, lane, bias, *pre, rs);
   } else {
     ARing<T, NT> own;
     ring_fill<T, NT>(own, W, wplane, ldw, nrow0, nkb, lane);
-    gemm_run<T, NT, MT>(W, wplane, ldw, nrow0, act, kc0, nkb, acc, lane, bias, own);
+    gemm_run<T, NT, MT, RSV>(W, wplane, ldw, nrow0, act, kc0, nkb, acc, lane, bias, own, rs);
   }
 }
 
@@ -1325,12 +1359,18 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   // the store's write acknowledgement too. The GEMM of layer l + 1 still reads H_l from the LDS tile, so H_l (and the
   // mask words of layer l) leave during iteration l + 1, between its GEMM and its epilogue barrier.
   uint64_t pbits[MW] = {};
+  // fp32: H_l's saved rows leave from the B fragments of the GEMM that reads H_l (YANERF_F32_GSAVE)
+  constexpr bool GS = std::is_same<T, float>::value && YANERF_F32_GSAVE && SAVE;
+  auto hsave = [&](int hl) {
+    return RowSave{(sv && hl >= 0) ? (float*)(void*)(saved + (SR.h0 + 256LL * hl) * ld + p0) : nullptr, soff,
+                   (int)ldb, (sv && hl >= 0) ? 256 / KB : 0, wave, WAVES};
+  };
   for (int l = 0; l < lay.L; ++l) {
     const bool sk = (lay.skip >> l) & 1u;
     const int kc0 = (l == 0) ? PE_COL / EPC : 0;
     const int nkb = (l == 0) ? KPE / KB : (sk ? 320 / KB : 256 / KB);
-    gemm_lds<T, NT, MT>(Wt + lay.w_off[l], wpl, lay.kpad[l], nrow0, act, kc0, nkb, acc, lane, Wf + lay.b_off[l],
-                        &ring);
+    gemm_lds<T, NT, MT, GS>(Wt + lay.w_off[l], wpl, lay.kpad[l], nrow0, act, kc0, nkb, acc, lane, Wf + lay.b_off[l],
+                            &ring, hsave(l - 1));
     if (l + 1 < lay.L)
       ring_fill<T, NT>(ring, Wt + lay.w_off[l + 1], wpl, lay.kpad[l + 1], nrow0, lay.kpad[l + 1] / KB, lane);
     else ring_fill<T, NT>(ring, Wt + lay.wint_off, wpl, 256, nrow0, 256 / KB, lane);
@@ -1358,7 +1398,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
         if (!(YANERF_ABLATE & 16)) pk_lds<T>(act, m, n, h);
         else if (__float_as_uint(acc[nt][mt].x) == 0x7fc00001u) act[m] = (LT)0;  // keep acc live
         if (sv && !(YANERF_ABLATE & 4)) {
-          if constexpr (!PM)
+          if constexpr (!PM && !GS)
             pk_store_rows_b<T>((saved + (SR.h0 + 256LL * l + nrow0 + 16 * nt) * ld + p0),
                                soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
           mask_acc(bits, h, nt * MT + mt);
@@ -1391,7 +1431,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     }
   }
   // ---- intermediate_linear (no activation)
-  gemm_lds<T, NT, MT>(Wt + lay.wint_off, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, Wf + lay.bint_off, &ring);
+  gemm_lds<T, NT, MT, GS>(Wt + lay.wint_off, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, Wf + lay.bint_off, &ring,
+                          hsave(lay.L - 1));
   const int crow0 = wave * NTC * 16;
   ARing<T, NTC> ringc;
   ring_fill<T, NTC>(ringc, Wt + lay.wc_off, wpl, KC, crow0, KC / KB, lane);
@@ -1692,6 +1733,9 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
     if (n > nb) dzc_part[(u * 2 + 1) * HC + c] = s1;
   }
   lds_barrier();
+  // fp32 with YANERF_F32_GSAVE_DX: dY and dZ_l (l >= 1) leave from the B fragments of the GEMM that reads them (as
+  // the forward's H rows), dZ_0 from the last epilogue. Off: measured dX 7.25 -> 7.50 ms (the forward gains 0.17 ms)
+  constexpr bool GSX = std::is_same<T, float>::value && YANERF_F32_GSAVE_DX;
   G8Max gmax;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
@@ -1703,7 +1747,7 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
       const Pk<T> h = pk_make<T>(v);
       if constexpr (PM && YANERF_BF16_G8) gmax.add(h);
       pk_lds<T>(act, m, n, h);
-      if constexpr (!PM)
+      if constexpr (!PM && !GSX)  // else stored by the first trunk step's GEMM
         pk_store_rows_b<T>((grad + (GR.dyx + nrow0 + 16 * nt) * ld + p0),
                              soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
     }
@@ -1722,7 +1766,9 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
 #pragma unroll
     for (int w = 0; w < MW; ++w)
       bits[w] = masks[((((int64_t)hl * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane];
-    gemm_lds<T, NT, MT>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring);
+    gemm_lds<T, NT, MT, GSX>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring,
+                             RowSave{(float*)(void*)(grad + (HEAD ? GR.dyx : GR.dz0 + 256LL * l) * ld + p0), soff,
+                                     (int)ldb, 256 / KB, wave, WAVES});
     if (l - 1 >= 1) ring_fill<T, NT, true>(ring, Wt + lay.wt_off[l - 1], wpl, 256, nrow0, 256 / KB, lane);
     // fp8 scale sets: dZc 0, dY 1, then dZ_{L-1}, dZ_{L-2}, ... alternate from set 0
     if constexpr (PM && !(YANERF_ABLATE & 128)) {  // the GEMM's input: dY (from the heads) or dZ_l
@@ -1751,7 +1797,7 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
         const Pk<T> h = pk_make<T>(apply_mask_tile<T, MW>(v, bits, nt * MT + mt));
         if constexpr (PM && YANERF_BF16_G8) gmax.add(h);
         pk_lds<T>(act, m, n, h);
-        if constexpr (!PM)
+        if (!PM && (!GSX || hl == 0))
           pk_store_rows_b<T>((grad + (GR.dz0 + 256LL * hl + nrow0 + 16 * nt) * ld + p0),
                              soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
       }
@@ -3196,7 +3242,9 @@ static int launch_fwd(const MlpLayout& L, int prec, const void* packed, const fl
   const float* Wf = (const float*)((const char*)packed + L.f_base);
   dim3 grid((unsigned)(Npad / Cfg<T>::M)), block(Cfg<T>::WAVES * 64);
   uint64_t* masks = saved ? (uint64_t*)((char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM)) : nullptr;
-  if (saved || !std::is_same<T, bf16_t>::value)
+  // bf16 and (with the in-GEMM saves) fp32 inference run the instantiation without the save code
+  constexpr bool SPLIT = std::is_same<T, bf16_t>::value || (std::is_same<T, float>::value && YANERF_F32_GSAVE);
+  if (saved || !SPLIT)
     hipLaunchKernelGGL((mlp_fwd_kernel<T, true>), grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, (ST*)saved,
                        saved ? masks : nullptr, Npad);
   else

@@ -865,14 +865,18 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
     if constexpr (RSV) {
       __builtin_amdgcn_sched_barrier(0);
       if (kb < rs.nkb && kb % rs.waves == rs.wave) {
-        char* rb = (char*)rs.base + (int64_t)(16 * kb) * rs.ldb;
+        // uniform 64-bit base of the K-block's 16 rows, 32-bit lane offsets (an opaque copy, so the compiler does not
+        // hoist 64-bit addresses for every K-block out of the caller's layer loop)
+        const char* rb = (const char*)rs.base + (int64_t)(16 * kb) * rs.ldb;
+        uint32_t vo = rs.voff;
+        asm volatile("" : "+v"(vo));
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          char* q = rb + 16 * mt * 4 + rs.voff;
-          *(float*)q = b[mt].x;
-          *(float*)(q + rs.ldb) = b[mt].y;
-          *(float*)(q + 2 * (int64_t)rs.ldb) = b[mt].z;
-          *(float*)(q + 3 * (int64_t)rs.ldb) = b[mt].w;
+          const uint32_t o = vo + 16 * mt * 4;
+          *(float*)(rb + o) = b[mt].x;
+          *(float*)(rb + o + (uint32_t)rs.ldb) = b[mt].y;
+          *(float*)(rb + o + 2u * (uint32_t)rs.ldb) = b[mt].z;
+          *(float*)(rb + o + 3u * (uint32_t)rs.ldb) = b[mt].w;
         }
       }
       __builtin_amdgcn_sched_barrier(0);

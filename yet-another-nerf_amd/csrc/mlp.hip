@@ -630,8 +630,11 @@ __device__ __forceinline__ void ring_fill(ARing<T, NT>& R, const typename Cfg<T>
 #define YANERF_F32_GSAVE 1
 #endif
 #ifndef YANERF_F32_GSAVE_DX
-#define YANERF_F32_GSAVE_DX 0
+#define YANERF_F32_GSAVE_DX 1
 #endif
+// RSV (gemm_run / gemm_lds template argument): 0 no row stores, 1 a K-block's stores after its MFMAs (the forward),
+// 2 before them (the dX kernel). Measured both ways in both kernels: forward 7.58 (after) vs 7.74 ms (before); dX
+// 7.29 (after) vs 6.88 ms (before), against 7.19 ms with epilogue stores.
 struct RowSave {
   float* base;    // saved row of the GEMM's feature 0 at the tile's first point
   uint32_t voff;  // this lane's byte offset in a 16x16 row tile (4g rows + li points)
@@ -640,7 +643,7 @@ struct RowSave {
   int wave, waves;
 };
 
-template <typename T, int NT, int MT, bool RSV = false>
+template <typename T, int NT, int MT, int RSV = 0>
 __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict__ W, int64_t wplane, int ldw, int nrow0,
                                          const typename Cfg<T>::lds_t* act, int kc0, int nkb, f4 (&acc)[NT][MT],
                                          int lane, const float* __restrict__ bias, ARing<T, NT>& R,
@@ -859,10 +862,29 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
     f4 b[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) b[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + kb * 4 + g);
+    if constexpr (RSV == 2) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (kb < rs.nkb && kb % rs.waves == rs.wave) {
+        // uniform 64-bit base of the K-block's 16 rows, 32-bit lane offsets (an opaque copy, so the compiler does not
+        // hoist 64-bit addresses for every K-block out of the caller's layer loop)
+        const char* rb = (const char*)rs.base + (int64_t)(16 * kb) * rs.ldb;
+        uint32_t vo = rs.voff;
+        asm volatile("" : "+v"(vo));
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const uint32_t o = vo + 16 * mt * 4;
+          *(float*)(rb + o) = b[mt].x;
+          *(float*)(rb + o + (uint32_t)rs.ldb) = b[mt].y;
+          *(float*)(rb + o + 2u * (uint32_t)rs.ldb) = b[mt].z;
+          *(float*)(rb + o + 3u * (uint32_t)rs.ldb) = b[mt].w;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if constexpr (YANERF_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     mma_grid<T, NT, MT>(a, b, acc);
     if constexpr (YANERF_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-    if constexpr (RSV) {
+    if constexpr (RSV == 1) {
       __builtin_amdgcn_sched_barrier(0);
       if (kb < rs.nkb && kb % rs.waves == rs.wave) {
         // uniform 64-bit base of the K-block's 16 rows, 32-bit lane offsets (an opaque copy, so the compiler does not
@@ -888,7 +910,7 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
 
 // gemm_run with a weight ring: `pre` was filled by the caller (ring_fill before the previous epilogue), else a local
 // one is filled here. (Two call paths, no pointer select, so the ring stays in registers.)
-template <typename T, int NT, int MT, bool RSV = false>
+template <typename T, int NT, int MT, int RSV = 0>
 __device__ __forceinline__ void gemm_lds(const typename Cfg<T>::w_t* __restrict__ W, int64_t wplane, int ldw, int nrow0,
                                          const typename Cfg<T>::lds_t* act, int kc0, int nkb, f4 (&acc)[NT][MT],
                                          int lane, const float* __restrict__ bias = nullptr,
@@ -1373,7 +1395,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     const bool sk = (lay.skip >> l) & 1u;
     const int kc0 = (l == 0) ? PE_COL / EPC : 0;
     const int nkb = (l == 0) ? KPE / KB : (sk ? 320 / KB : 256 / KB);
-    gemm_lds<T, NT, MT, GS>(Wt + lay.w_off[l], wpl, lay.kpad[l], nrow0, act, kc0, nkb, acc, lane, Wf + lay.b_off[l],
+    gemm_lds<T, NT, MT, GS ? 1 : 0>(Wt + lay.w_off[l], wpl, lay.kpad[l], nrow0, act, kc0, nkb, acc, lane, Wf + lay.b_off[l],
                             &ring, hsave(l - 1));
     if (l + 1 < lay.L)
       ring_fill<T, NT>(ring, Wt + lay.w_off[l + 1], wpl, lay.kpad[l + 1], nrow0, lay.kpad[l + 1] / KB, lane);
@@ -1435,7 +1457,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     }
   }
   // ---- intermediate_linear (no activation)
-  gemm_lds<T, NT, MT, GS>(Wt + lay.wint_off, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, Wf + lay.bint_off, &ring,
+  gemm_lds<T, NT, MT, GS ? 1 : 0>(Wt + lay.wint_off, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, Wf + lay.bint_off, &ring,
                           hsave(lay.L - 1));
   const int crow0 = wave * NTC * 16;
   ARing<T, NTC> ringc;
@@ -1737,8 +1759,9 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
     if (n > nb) dzc_part[(u * 2 + 1) * HC + c] = s1;
   }
   lds_barrier();
-  // fp32 with YANERF_F32_GSAVE_DX: dY and dZ_l (l >= 1) leave from the B fragments of the GEMM that reads them (as
-  // the forward's H rows), dZ_0 from the last epilogue. Off: measured dX 7.25 -> 7.50 ms (the forward gains 0.17 ms)
+  // fp32 (YANERF_F32_GSAVE_DX): dY and dZ_l (l >= 1) leave from the B fragments of the GEMM that reads them, each
+  // K-block's stores BEFORE its MFMAs (RSV 2; after them, as the forward does, measured slower here); dZ_0 from the
+  // last epilogue
   constexpr bool GSX = std::is_same<T, float>::value && YANERF_F32_GSAVE_DX;
   G8Max gmax;
 #pragma unroll
@@ -1770,7 +1793,7 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
 #pragma unroll
     for (int w = 0; w < MW; ++w)
       bits[w] = masks[((((int64_t)hl * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane];
-    gemm_lds<T, NT, MT, GSX>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring,
+    gemm_lds<T, NT, MT, GSX ? 2 : 0>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring,
                              RowSave{(float*)(void*)(grad + (HEAD ? GR.dyx : GR.dz0 + 256LL * l) * ld + p0), soff,
                                      (int)ldb, 256 / KB, wave, WAVES});
     if (l - 1 >= 1) ring_fill<T, NT, true>(ring, Wt + lay.wt_off[l - 1], wpl, 256, nrow0, 256 / KB, lane);

@@ -311,6 +311,53 @@ def psnr_leg(precision: str, steps: int, dev):
     return r
 
 
+def distributed_fields(dt_local: float, steps: int, exposed_ms, exchange: str, dev=None) -> dict:
+    """What an N-rank line must show (SCALE runs): the process group's backend and size as the group itself reports
+    them, every rank's own ms/step (min / max / all), and the exposed part of the gradient exchange per step (HIP
+    events on the compute stream around the wait for the all-reduce; per rank, then max and mean over ranks).
+    Reference: the DDP setup of scripts/run.py:162-166 and runners/utils.py:216-238."""
+    import torch.distributed as dist
+    ms = parallel.allgather_floats(1e3 * dt_local / steps, device=dev)
+    ex = parallel.allgather_floats(float("nan") if exposed_ms is None else float(exposed_ms), device=dev)
+    return {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "grad_exchange": exchange,
+            "ms_per_step_per_rank": [round(v, 4) for v in ms], "ms_per_step_min": round(min(ms), 4),
+            "ms_per_step_max": round(max(ms), 4),
+            "allreduce_exposed_ms_per_rank": [round(v, 4) for v in ex],
+            "allreduce_exposed_ms_max": round(max(ex), 4), "allreduce_exposed_ms_mean": round(sum(ex) / len(ex), 4),
+            "grad_bytes": 4 * 1_191_688}
+
+
+def dist_selftest(steps: int) -> None:
+    """`--dist-selftest`: the N-rank plumbing of this script without the GPU (CPU ranks over gloo under
+    torch.distributed.run): the trainer's two-bucket exchange of the Lego-size flat gradient (1,191,688 fp32) timed
+    for `steps` steps, then the same `distributed` fields the real run reports. Not a measurement of anything."""
+    rank, world, _ = parallel.init_distributed(backend="gloo")
+    n, n_coarse = 1_191_688, 595_844
+    grad = torch.full((n,), float(rank + 1))
+    parallel.barrier()
+    t0 = time.perf_counter()
+    ex = 0.0
+    for _ in range(steps):
+        h = parallel.allreduce_sum_async(grad[:n_coarse])
+        h2 = parallel.allreduce_sum_async(grad[n_coarse:])
+        t1 = time.perf_counter()
+        parallel.finish_allreduce(h)
+        parallel.finish_allreduce(h2)
+        ex += time.perf_counter() - t1
+        grad.div_(world)
+    dt = time.perf_counter() - t0
+    info = distributed_fields(dt, steps, 1e3 * ex / steps, "bucketed")
+    expect = sum(range(1, world + 1)) / world  # the first step's mean; later steps average identical values
+    info["selftest_grad_ok"] = bool(torch.allclose(grad, torch.full_like(grad, expect)))
+    if rank == 0:
+        print(json.dumps({"selftest": True, "n_gpus": world, "distributed": info}))
+    parallel.barrier()
+    torch.distributed.destroy_process_group()
+
+
+LEGO_TRAIN_IMAGES = 100  # nerf_synthetic Lego's train split (the loader length scripts/run.py:243-271 converts with)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -326,7 +373,11 @@ def main():
     ap.add_argument("--psnr-steps", type=int, default=1000,
                     help="train this many steps on the procedural nerf_synthetic-format scene and report its test PSNR "
                          "(rank 0 at N=1; 0 = skip)")
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="CPU/gloo check of the N-rank plumbing and its JSON fields (no GPU work; not a benchmark)")
     args = ap.parse_args()
+    if args.dist_selftest:
+        return dist_selftest(args.steps)
 
     rank, world, local = parallel.init_distributed()
     if world != args.gpus and rank == 0:
@@ -345,12 +396,15 @@ def main():
     focal = torch.tensor([focal_px], device=dev)
 
     def run(precision: str, steps: int, warmup: int, probes: bool):
-        # the reference runner's schedule (warm-up, exponential decay; init/min lr scaled by the world size)
-        tr = NeRFTrainer(pcfg, precision=precision, device=dev, runner_cfg=cfg.runner, n_rays=args.rays)
+        # the reference runner's schedule (warm-up, exponential decay; init/min lr scaled by the world size), after
+        # scripts/run.py's iteration -> epoch conversion over Lego's 100 training images at this world size
+        tr = NeRFTrainer(pcfg, precision=precision, device=dev, runner_cfg=cfg.runner, n_rays=args.rays,
+                         train_set_size=LEGO_TRAIN_IMAGES)
         for i in range(warmup):
             tr.step(poses[(i + rank) % len(poses)][None], focal, image)
-        if probes:  # HIP events around the two forward launches (they have the GPU to themselves)
-            tr.enable_probes(["mlp_fwd_0", "mlp_fwd_1"])
+        if probes:  # HIP events around the two forward launches (they have the GPU to themselves) and, at N > 1,
+            # around the wait for the gradient exchange on the compute stream (its exposed part)
+            tr.enable_probes(["mlp_fwd_0", "mlp_fwd_1"] + (["allreduce_exposed"] if world > 1 else []))
         parallel.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -359,11 +413,15 @@ def main():
             out = tr.step(poses[(warmup + i + rank) % len(poses)][None], focal, image)
         torch.cuda.synchronize()
         parallel.barrier()
-        dt = parallel.max_over_ranks(time.perf_counter() - t0, device=dev)
+        dt_local = time.perf_counter() - t0
+        dt = parallel.max_over_ranks(dt_local, device=dev)
         mse_f = float(out["sq_fine"].mean().item() / 3.0)
+        tr.dt_local = dt_local
         return tr, dt, mse_f
 
     tr, dt, mse_f = run(args.precision, args.steps, args.warmup, probes=True)
+    dist_info = distributed_fields(tr.dt_local, args.steps, tr.probe_ms().get("allreduce_exposed"), tr.grad_exchange,
+                                   dev) if world > 1 else None
     R, Pc, Pf = tr.R, tr.Pc, tr.Pf
     rays_total = R * world * args.steps
     value = rays_total / dt
@@ -393,9 +451,11 @@ def main():
         "roofline_kernels": rk,
         "step_mfma_tflops": round(flops_ray * value / world / 1e12, 2),
         "step_mfma_frac": round(flops_ray * value / world / 1e12 / peak, 4),
-        "fwd_ms_in_timed_steps": {k: round(v, 4) for k, v in probe.items()},
+        "fwd_ms_in_timed_steps": {k: round(v, 4) for k, v in probe.items() if k.startswith("mlp_")},
         "kernel_ms_serialised": serial_ms,
     }
+    if dist_info is not None:
+        result["distributed"] = dist_info
     del tr
     # the other precision modes on the same workload, reported beside the headline (never in `value`)
     notes = {"bf16": "throughput mode: bf16 weights/activations, fp32 accumulate; parity-gated only loosely",

@@ -37,6 +37,10 @@ extern "C" {
 
 const char* yanerf_last_error(void);
 int yanerf_version(void);
+/* First 16 hex digits of the SHA-256 of the sources this library was compiled from (render.hip, mlp.hip,
+   common.hpp, this header, the Makefile, in that order): the Python binding refuses a library whose id does not
+   match the sources beside it (a stale prebuilt .so). Not a reference entry point. */
+const char* yanerf_build_id(void);
 
 /* ------------------------------------------------------------------------------------------------
  * Ray generation. Replaces _RaySampler.forward + _xy_to_ray_bundle + _jiggle_within_stratas
@@ -54,12 +58,15 @@ int yanerf_version(void);
  *     1 = injected uniforms jitter_u [B][R][P], 2 = Philox(seed, offset).
  *   Outputs: origins [B][R][3], directions [B][R][3] (unnormalised, as the reference), lengths
  *     [B][R][P], xys [B][R][2]; ids_out [B][R] (may be NULL).
+ *   bounds: NULL, or 2 device floats (near, far) that replace near/far -- LLFF's per-image bounds averaged on the
+ *     device (ray_sampler.py:280-283 reads them with .item(), a host sync per step).
+ *   rng_base: NULL, or 1 device u64 added to `offset` (a graph-captured step advances it on the device).
  * ---------------------------------------------------------------------------------------------- */
 int yanerf_raygen(const float* poses, const float* focal, const float* xy, const int64_t* pixel_ids,
                   int64_t B, int64_t R, int64_t grid_w, int64_t grid_h, float cfg_w, float cfg_h,
                   float near, float far, int64_t P, int jitter_mode, const float* jitter_u,
                   uint64_t seed, uint64_t offset, float* origins, float* directions, float* lengths,
-                  float* xys, int64_t* ids_out, void* stream);
+                  float* xys, int64_t* ids_out, const float* bounds, const uint64_t* rng_base, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
  * NeRF MLP (NeRFMLP.forward, yanerf/pipelines/models/nerf_mlp.py:117-177, incl. MLPWithInputSkips
@@ -134,6 +141,7 @@ typedef struct yanerf_raymarch_opts {
   int32_t noise_mode;       /* 0 none, 1 injected normals noise[R][P], 2 Philox(seed, offset) normals  */
   float noise_std;          /* density_noise_std (renderer.py:204-205)                                */
   uint64_t seed, offset;
+  const uint64_t* rng_base; /* NULL, or a device u64 added to offset (graph replay)                   */
 } yanerf_raymarch_opts;
 
 /* sigma_raw [R][P], rgb [R][P][C], lengths [R][P], directions [R][3], bg [R][C] or NULL,
@@ -176,7 +184,7 @@ int yanerf_sample_pdf(const float* bins, const float* weights, int64_t R, int64_
  * [R][n_fine]: midpoints (torch.lerp(z[1:], z[:-1], 0.5)), sample_pdf on ray_weights[..., 1:-1], merge. */
 int yanerf_refine(const float* lengths, const float* ray_weights, int64_t R, int64_t P, int64_t n_fine,
                   int det, const float* u, uint64_t seed, uint64_t offset, int add_input,
-                  float* lengths_out, void* stream);
+                  float* lengths_out, const uint64_t* rng_base, void* stream);
 
 /* ------------------------------------------------------------------------------------------------
  * Photometric loss of the training objective (pipelines/utils.py:189-196; nerf_pipeline.py:284-305):

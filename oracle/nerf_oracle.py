@@ -182,6 +182,10 @@ class MLPCache:
     rgb: np.ndarray = None
     n_rays: int = 0
     P: int = 0
+    layer_pre: List[np.ndarray] = field(default_factory=list)  # trunk pre-activations (before the ReLU)
+    c0_pre: np.ndarray = None  # colour hidden pre-activation
+    trunk_masks: Optional[List[np.ndarray]] = None  # the ReLU decisions used (None: the activations' own, y > 0)
+    color_mask: Optional[np.ndarray] = None
 
 
 def linear(x, W, b):
@@ -191,11 +195,22 @@ def linear(x, W, b):
     return y.astype(f32)
 
 
-def nerf_mlp_forward(params: Dict[str, np.ndarray], arch: MLPArch, origins, directions, lengths, code=None):
+def _relu_with(z: np.ndarray, mask: Optional[np.ndarray]) -> np.ndarray:
+    """relu(z), or -- with an injected ReLU decision per unit -- z where mask, 0 elsewhere."""
+    return relu(z) if mask is None else np.where(mask, z, f32(0.0)).astype(f32)
+
+
+def nerf_mlp_forward(params: Dict[str, np.ndarray], arch: MLPArch, origins, directions, lengths, code=None,
+                     relu_masks: Optional[dict] = None):
     """NeRFMLP.forward (nerf_mlp.py:117-177) with MLPWithInputSkips (nerf_mlp.py:267-289) and
     LinearWithRepeat (models/utils.py:207-211). origins/directions (..., 3), lengths (..., P).
     `code` (latent_dim,): one batch element's global code, appended to every point's xyz embedding
     (create_embeddings_for_implicit_function / broadcast_global_code, nerf_mlp.py:299-335).
+    relu_masks (test support): {"trunk": [n_layers bool (R*P, hidden)], "color": bool (R*P, hidden_dir)} -- the
+    ReLU decisions of another fp32 evaluation of the same network (the reference's, recorded in the golden, or the
+    HIP kernels'), used instead of this evaluation's own signs, forward and backward: a pre-activation within
+    rounding of zero can fall on either side of the kink in two correct fp32 implementations, and with it that
+    unit's whole gradient contribution (tests/parity_gates.py).
     Returns sigma (..., P, 1), rgb (..., P, C), cache."""
     lead = lengths.shape[:-1]
     P = lengths.shape[-1]
@@ -208,12 +223,17 @@ def nerf_mlp_forward(params: Dict[str, np.ndarray], arch: MLPArch, origins, dire
     if code is not None:
         embed = np.concatenate([embed, np.broadcast_to(np.asarray(code, f32), (R * P, len(code)))], -1)
     cache = MLPCache(embed=embed, n_rays=R, P=P)
+    if relu_masks is not None:
+        cache.trunk_masks = [np.asarray(m, bool).reshape(R * P, -1) for m in relu_masks["trunk"]]
+        cache.color_mask = np.asarray(relu_masks["color"], bool).reshape(R * P, -1)
     y = embed
     for li in range(arch.n_layers):
         if li in arch.input_skips:
             y = np.concatenate([y, embed], -1)
         cache.layer_in.append(y)
-        y = relu(linear(y, params[f"xyz_encoder.mlp.{li}.0.weight"], params[f"xyz_encoder.mlp.{li}.0.bias"]))
+        z = linear(y, params[f"xyz_encoder.mlp.{li}.0.weight"], params[f"xyz_encoder.mlp.{li}.0.bias"])
+        cache.layer_pre.append(z)
+        y = _relu_with(z, None if cache.trunk_masks is None else cache.trunk_masks[li])
         cache.layer_out.append(y)
     feats = y
     cache.features = feats
@@ -226,7 +246,9 @@ def nerf_mlp_forward(params: Dict[str, np.ndarray], arch: MLPArch, origins, dire
     n1 = inter.shape[-1]
     out1 = linear(inter, Wc[:, :n1], params["color_layer.0.bias"]).reshape(R, P, -1)
     out2 = linear(dir_embed, Wc[:, n1:], None)
-    c0 = relu((out1 + out2[:, None, :]).astype(f32)).reshape(R * P, -1)
+    c0_pre = (out1 + out2[:, None, :]).astype(f32).reshape(R * P, -1)
+    cache.c0_pre = c0_pre
+    c0 = _relu_with(c0_pre, cache.color_mask)
     cache.c0 = c0
     rgb = sigmoid(linear(c0, params["color_layer.2.weight"], params["color_layer.2.bias"]))
     cache.rgb = rgb
@@ -246,7 +268,7 @@ def nerf_mlp_backward(params: Dict[str, np.ndarray], arch: MLPArch, cache: MLPCa
     grads["color_layer.2.weight"] = (gu.T @ cache.c0).astype(f32)
     grads["color_layer.2.bias"] = gu.sum(0).astype(f32)
     gc0 = (gu @ params["color_layer.2.weight"]).astype(f32)
-    gz = np.where(cache.c0 > 0, gc0, f32(0.0)).astype(f32)
+    gz = np.where(cache.c0 > 0 if cache.color_mask is None else cache.color_mask, gc0, f32(0.0)).astype(f32)
     n1 = cache.inter.shape[-1]
     gW1 = (gz.T @ cache.inter).astype(f32)
     gz_ray = gz.reshape(R, P, -1).sum(1).astype(f32)
@@ -261,7 +283,7 @@ def nerf_mlp_backward(params: Dict[str, np.ndarray], arch: MLPArch, cache: MLPCa
     gy = (g_inter @ params["intermediate_linear.weight"] + gs @ params["density_layer.weight"]).astype(f32)
     for li in reversed(range(arch.n_layers)):
         y = cache.layer_out[li]
-        gzl = np.where(y > 0, gy, f32(0.0)).astype(f32)
+        gzl = np.where(y > 0 if cache.trunk_masks is None else cache.trunk_masks[li], gy, f32(0.0)).astype(f32)
         W = params[f"xyz_encoder.mlp.{li}.0.weight"]
         grads[f"xyz_encoder.mlp.{li}.0.weight"] = (gzl.T @ cache.layer_in[li]).astype(f32)
         grads[f"xyz_encoder.mlp.{li}.0.bias"] = gzl.sum(0).astype(f32)
@@ -455,16 +477,21 @@ class RenderCfg:
 
 
 def render_two_pass(params_c, params_f, arch, cfg: RenderCfg, origins, directions, lengths, bg=None,
-                    noise_c=None, noise_f=None, pdf_u=None, random_sampling=False):
+                    noise_c=None, noise_f=None, pdf_u=None, random_sampling=False, z_fine=None, relu_masks=None):
     """MultipassEmissionAbsorpsionRenderer._run_raymarcher recursion (renderer.py:84-117) for 2 passes.
-    origins/directions (R,3), lengths (R,Pc). Returns dict with both stages and caches."""
+    origins/directions (R,3), lengths (R,Pc). z_fine (optional): the refined depths to run the fine pass at instead
+    of this refinement (e.g. the reference's own, recorded in the golden). relu_masks (optional): (coarse, fine)
+    ReLU decisions for nerf_mlp_forward. Returns dict with both stages and caches."""
     R = lengths.shape[0]
-    sc, cc, cache_c = nerf_mlp_forward(params_c, arch, origins, directions, lengths)
+    mc, mf = relu_masks if relu_masks is not None else (None, None)
+    sc, cc, cache_c = nerf_mlp_forward(params_c, arch, origins, directions, lengths, relu_masks=mc)
     fc, dc, ac, wc, ctx_c = raymarch_forward(sc, cc, lengths, directions, cfg.raymarch,
                                              noise=None if noise_c is None else noise_c.reshape(R, -1),
                                              bg=bg, default_bg=cfg.bg_color)
-    zf = refine(lengths, wc, cfg.n_pts_fine, random_sampling, u=pdf_u, add_input_samples=cfg.append_coarse_samples_to_fine)
-    sf, cf, cache_f = nerf_mlp_forward(params_f, arch, origins, directions, zf)
+    zf = refine(lengths, wc, cfg.n_pts_fine, random_sampling, u=pdf_u,
+                add_input_samples=cfg.append_coarse_samples_to_fine) if z_fine is None else \
+        np.asarray(z_fine, f32).reshape(R, -1)
+    sf, cf, cache_f = nerf_mlp_forward(params_f, arch, origins, directions, zf, relu_masks=mf)
     ff, df, af, wf, ctx_f = raymarch_forward(sf, cf, zf, directions, cfg.raymarch,
                                              noise=None if noise_f is None else noise_f.reshape(R, -1),
                                              bg=bg, default_bg=cfg.bg_color)
@@ -473,12 +500,13 @@ def render_two_pass(params_c, params_f, arch, cfg: RenderCfg, origins, direction
 
 
 def train_step_grads(params_c, params_f, arch, cfg: RenderCfg, origins, directions, lengths, gt_rgb,
-                     noise_c, noise_f, pdf_u):
+                     noise_c, noise_f, pdf_u, z_fine=None, relu_masks=None):
     """One training step's objective and parameter gradients (nerf_pipeline.py:181-213, 284-305; apis.py:87-88):
     objective = mse(fine) + mse(coarse); noise_* already include density_noise_std."""
     R = lengths.shape[0]
     out = render_two_pass(params_c, params_f, arch, cfg, origins, directions, lengths, noise_c=noise_c,
-                          noise_f=noise_f, pdf_u=pdf_u, random_sampling=True)
+                          noise_f=noise_f, pdf_u=pdf_u, random_sampling=True, z_fine=z_fine,
+                          relu_masks=relu_masks)
     gt = gt_rgb.reshape(R, 3)
     mse_f = rgb_metrics(gt[None], out["fine"][0][None])["rgb_mse"]
     mse_c = rgb_metrics(gt[None], out["coarse"][0][None])["rgb_mse"]

@@ -313,18 +313,49 @@ def gen_train_step(out):
     g = torch.Generator().manual_seed(8)
     img = torch.rand(1, 800, 800, 3, generator=g)
     rec = Recorder()
+    # the refiner's input weights and output depths (RayPointRefiner.forward, renderers/utils.py:48-69; the fine pass
+    # runs at these depths, multipass_emission_absorpsion_renderer.py:107-114): recorded through a pass-through wrapper
+    refined = []
+    orig_fwd = RayPointRefiner.forward
+
+    def rec_fwd(self, origins, directions, lengths, xys, ray_weights):
+        rb = orig_fwd(self, origins, directions, lengths, xys, ray_weights)
+        refined.append((ray_weights.detach().clone(), rb.lengths.detach().clone()))
+        return rb
+
+    RayPointRefiner.forward = rec_fwd
+    # the ReLU decisions of both MLPs (output > 0 of every ReLU module: the 8 trunk layers, nerf_mlp.py:256-260, and
+    # the colour hidden layer, :72-83), per point, so a parity test can tell an fp32 tie at a kink from an error
+    relu = {}
+    hooks = []
+    for k, f in enumerate(pipe.implicit_functions):
+        mods = [(f"{k}:trunk{li}", layer[1]) for li, layer in enumerate(f._fn.xyz_encoder.mlp)]
+        mods.append((f"{k}:color", f._fn.color_layer[1]))
+        for key, mod in mods:
+            hooks.append(mod.register_forward_hook(
+                lambda m, i, o, key=key: relu.__setitem__(key, (o.detach() > 0).reshape(-1, o.shape[-1]).numpy())))
     torch.manual_seed(10)
-    with rec.capture():
-        preds = pipe(poses=pose, focal_lengths=focal, image_rgb=img, evaluation_mode=EvaluationMode.TRAINING)
+    try:
+        with rec.capture():
+            preds = pipe(poses=pose, focal_lengths=focal, image_rgb=img, evaluation_mode=EvaluationMode.TRAINING)
+    finally:
+        RayPointRefiner.forward = orig_fwd
+        for h in hooks:
+            h.remove()
     preds["objective"].mean().backward()
     ids = rec.take("multinomial")[0].numpy().astype(np.int64)
+    assert len(refined) == 1
     d = dict(pose=np32(pose), focal=np32(focal), seeds=np.array([21, 22]), n_rays=np.int64(n_rays),
              pixel_ids=ids, gt_rgb=np32(img.reshape(1, -1, 3)[0, ids[0]]),
              jitter_u=np32(rec.take("rand_like")[0]),
              noise_coarse=np32(rec.take("randn_like")[0]), noise_fine=np32(rec.take("randn_like")[1]),
-             pdf_u=np32(rec.take("rand")[0]))
+             pdf_u=np32(rec.take("rand")[0]),
+             coarse_weights=np32(refined[0][0]).reshape(n_rays, -1), z_fine=np32(refined[0][1]).reshape(n_rays, -1))
     for k in ("objective", "loss_rgb_mse", "loss_prev_stage_rgb_mse", "loss_rgb_huber"):
         d[k] = np32(preds[k])
+    for k in range(len(pipe.implicit_functions)):  # bit-packed along the feature axis (np.packbits, big-endian)
+        d[f"relu{k}:trunk"] = np.stack([np.packbits(relu[f"{k}:trunk{li}"], axis=-1) for li in range(8)])
+        d[f"relu{k}:color"] = np.packbits(relu[f"{k}:color"], axis=-1)
     for i, f in enumerate(pipe.implicit_functions):
         for name, p in f._fn.named_parameters():
             gr = np32(p.grad)
@@ -510,9 +541,69 @@ def gen_lr_schedule(out):
     out["lr_schedule"] = d
 
 
+ITER_RUNNER_CASES = {  # tag: (config file, runner overrides, train images, world size, batch size)
+    "lego_w1": ("configs/nerf/lego.yml", {}, 100, 1, 1),
+    "lego_w8": ("configs/nerf/lego.yml", {}, 100, 8, 1),
+    "lego_w3": ("configs/nerf/lego.yml", {}, 100, 3, 1),
+    "lego_cos_w2_b2": ("configs/nerf/lego.yml", {"lr_decay_type": "cosine"}, 100, 2, 2),
+    "fern_w1": ("configs/nerf/fern.yml", {}, 17, 1, 1),
+    "fern_w4": ("configs/nerf/fern.yml", {}, 17, 4, 1),
+    "fern_w8": ("configs/nerf/fern.yml", {}, 17, 8, 1),
+}
+ITER_RUNNER_KEYS = ("num_iters", "num_iters_on_one_gpu", "num_epochs", "val_per_epoch", "save_per_epoch",
+                    "lr_decay_iters", "val_per_iter", "save_per_iter")
+
+
+def gen_iter_runner(out):
+    """scripts/run.py:243-271 setup_iter_based_runner (the iteration -> epoch conversion that rescales every '*iters'
+    key of the runner config before the scheduler is built, run.py:144), run by the reference itself on its product
+    configs at several world sizes: the training DataLoader is the one create_loader builds (DistributedSampler over
+    the train split, drop_last=True; runners/utils.py:112-145) over a dummy dataset of the split's size, and
+    get_world_size is pinned to the world size. Then the per-iteration learning rate under the rescaled config with
+    the linear world scaling (run.py:152-156), through the reference's create_lr_scheduler + warmup_lr_scheduler."""
+    import importlib.util
+    import logging
+
+    from torch.utils.data import DistributedSampler
+
+    from yanerf.runners.utils import create_loader, create_lr_scheduler, warmup_lr_scheduler
+    spec = importlib.util.spec_from_file_location("ref_scripts_run", REF / "scripts" / "run.py")
+    run = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(run)
+    log = logging.getLogger("golden")
+    its = np.unique(np.concatenate([np.arange(0, 1010), np.arange(1010, 40000, 37), np.arange(40000, 260000, 997)]))
+    d = dict(iters=its.astype(np.int64), keys=np.array(ITER_RUNNER_KEYS))
+    for tag, (cfgfile, over, n_train, world, bs) in ITER_RUNNER_CASES.items():
+        cfg = Config.fromfile(str(REF / cfgfile))
+        for k, v in over.items():
+            cfg.runner[k] = v
+        ds = list(range(n_train))
+        sampler = DistributedSampler(ds, num_replicas=world, rank=0, shuffle=True) if world > 1 else None
+        dl = create_loader(ds, sampler, batch_size=bs, num_workers=0, is_train=True)
+        run.get_world_size = lambda w=world: w
+        run.setup_iter_based_runner(cfg.runner, dl, log)
+        d[f"{tag}:case"] = np.array([cfgfile, repr(over), str(n_train), str(world), str(bs)])
+        d[f"{tag}:len_loader"] = np.int64(len(dl))
+        d[f"{tag}:values"] = np.array([float(cfg.runner[k]) for k in ITER_RUNNER_KEYS], np.float64)
+        r = cfg.runner
+        if world > 1 and r.linear_scale:  # scripts/run.py:152-156
+            r.init_lr, r.min_lr = r.init_lr * world, r.min_lr * world
+        p = torch.nn.Parameter(torch.zeros(1))
+        opt = torch.optim.Adam([{"params": [p], "init_lr": r.init_lr}], lr=r.init_lr)
+        sched = create_lr_scheduler(opt, r)
+        lrs = []
+        for it in its.tolist():
+            sched(iter=it)
+            if r["warmup_steps"] > 0 and it <= r["warmup_steps"]:
+                warmup_lr_scheduler(opt, it, r["warmup_steps"], r["warmup_lr"])
+            lrs.append(opt.param_groups[0]["lr"])
+        d[f"{tag}:lr"] = np.array(lrs, np.float64)
+    out["iter_runner"] = d
+
+
 GENERATORS = (gen_harmonic, gen_raysampler, gen_mlp, gen_raymarcher, gen_sample_pdf, gen_render_eval,
               gen_train_step, gen_zero_outputer, gen_init_checksums, gen_pipeline_state, gen_lr_schedule,
-              gen_raysampler_masked)
+              gen_raysampler_masked, gen_iter_runner)
 
 
 def main():

@@ -90,9 +90,9 @@ def test_argument_validation_returns_error_without_launch():
     assert L.yanerf_composite_forward(ctypes.byref(o), None, None, None, None, None, None, 4, 1000, 3, None, None,
                                       None, None, None) == 1
     assert "P=1000" in L.yanerf_last_error().decode()
-    assert L.yanerf_refine(None, None, 4, 2, 8, 1, None, 0, 0, 1, None, None) == 1
+    assert L.yanerf_refine(None, None, 4, 2, 8, 1, None, 0, 0, 1, None, None, None) == 1
     assert L.yanerf_raygen(None, None, None, None, 1, 1, 1, 1, 1.0, 1.0, 0.0, 1.0, 4, 0, None, 0, 0, None, None, None,
-                           None, None, None) == 1
+                           None, None, None, None, None) == 1
 
 
 def test_mlp_backward_phase_validation():
@@ -108,3 +108,21 @@ def test_mlp_backward_phase_validation():
     args[2] = None
     assert L.yanerf_mlp_backward_phase(*args, 1, None) == 1
     assert "null" in L.yanerf_last_error().decode()
+
+
+def test_composite_noise_mode_needs_noise():
+    """noise_mode 1 (injected density noise) with a null noise pointer is an argument error in every composite entry
+    point (no launch, so no device null dereference)."""
+    L = _C.lib()
+    o = _C.RaymarchOpts()
+    o.bg_default_n = 1
+    o.noise_mode = 1
+    d = ctypes.c_void_p(16)
+    assert L.yanerf_composite_forward(ctypes.byref(o), d, d, d, d, None, None, 4, 8, 3, d, d, d, d, None) == 1
+    assert "needs noise" in L.yanerf_last_error().decode()
+    assert L.yanerf_composite_backward(ctypes.byref(o), d, d, d, d, None, None, d, None, None, 4, 8, 3, d, d,
+                                       None) == 1
+    assert "needs noise" in L.yanerf_last_error().decode()
+    assert L.yanerf_composite_train(ctypes.byref(o), d, d, d, d, None, None, d, d, 1, 4, 8, 3, 8, 8, 1.0, d, d, d, d,
+                                    d, d, d, d, None) == 1
+    assert "needs noise" in L.yanerf_last_error().decode()

@@ -248,3 +248,19 @@ def test_ddp_registry_pipeline_two_ranks():
     assert not torch.equal(la, lb)
     assert torch.equal(ra, rb)
     np.testing.assert_allclose(ra.numpy(), mean.numpy(), rtol=0, atol=1e-7 * float(mean.abs().max()))
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_card_reports_distributed_fields():
+    """The real bench (fused training step, RCCL replaced by gloo because two ranks share the one card of a test box)
+    under torch.distributed.run with 2 ranks: the N-rank line has the process group's backend and world size, both
+    ranks' ms/step and the exposed gradient exchange (HIP events around the wait), and value = both ranks' rays / the
+    max-over-ranks time. Not a measurement (the ranks share one GPU)."""
+    from test_parallel import _run_bench_dist
+    d = _run_bench_dist(["--steps", "3", "--warmup", "1", "--psnr-steps", "0", "--secondary", "none", "--no-extras",
+                         "--no-cpu-baseline", "--rays", "1024"], timeout=600, env={"YANERF_DIST_BACKEND": "gloo"})
+    info = d["distributed"]
+    assert d["n_gpus"] == 2 and info["backend"] == "gloo" and info["world_size"] == 2
+    assert len(info["ms_per_step_per_rank"]) == 2 and all(v > 0 for v in info["ms_per_step_per_rank"])
+    assert info["allreduce_exposed_ms_max"] >= 0.0
+    np.testing.assert_allclose(d["value"], 2 * 1024 * 3 / (d["ms_per_step"] * 3 / 1e3), rtol=1e-3)

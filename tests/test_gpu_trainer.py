@@ -14,7 +14,8 @@ import pytest
 import torch
 
 from oracle import nerf_oracle as O
-from parity_gates import oracle_fine_at, split_gate
+from parity_gates import (STRICT_GRAD, TIE_REL, golden_grad_pairs, golden_relu_masks, grad_err, hip_relu_masks,
+                          loose_grad_gate, oracle_fine_at, relu_ties, split_gate, write_report)
 from weights import LEGO_ARCH, make_nerf_mlp_params
 
 pytestmark = pytest.mark.gpu
@@ -28,12 +29,6 @@ def t(x, dtype=torch.float32):
 
 def n(x):
     return x.detach().float().cpu().numpy()
-
-
-def close_frac(a, b, tol, frac, hard):
-    err = np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64))
-    assert err.max() <= hard, f"max err {err.max():.3e} > {hard:.3e}"
-    assert (err <= tol).mean() >= frac, f"only {(err <= tol).mean():.4f} within {tol:.3e}"
 
 
 def lego_cfg():
@@ -58,16 +53,47 @@ def make_trainer(precision, seeds, n_rays=256, **kw):
 
 
 # ------------------------------------------------------------------------------------------- training step
+def lego_oracle_inputs(g):
+    """The golden training step's rays, targets and scaled noise, as the oracle takes them (test_oracle_golden)."""
+    R = int(g["n_rays"])
+    o, d, z, _ = O.sample_rays_train(g["pose"], g["focal"], 800, 800, 2.0, 6.0, 64, g["pixel_ids"], g["jitter_u"])
+    return (o.reshape(R, 3), d.reshape(R, 3), z.reshape(R, 64), g["gt_rgb"],
+            (g["noise_coarse"] * np.float32(0.2)).astype(np.float32),
+            (g["noise_fine"] * np.float32(0.2)).astype(np.float32), g["pdf_u"])
+
+
+LEGO_TRAIN_CFG = O.RenderCfg(n_pts_fine=128, density_noise_std=0.2, raymarch=O.RaymarchOpts(background_density_bias=1e-6))
+
+
+@pytest.mark.parametrize("depths", ["reference", "own"])
 @pytest.mark.parametrize("precision", ["fp32", "fp32x3"])
-def test_trainer_step_matches_reference_step(golden, precision):
+def test_trainer_step_matches_reference_step(golden, precision, depths):
+    """The benched step (NeRFTrainer.step) replays the reference's training step (train_step_lego.npz: its pixel ids,
+    jitter, both density-noise draws and refinement uniforms injected), and every one of the 48 gradient tensors is
+    held to 1e-4 * max ELEMENTWISE, with nothing statistical:
+
+    * depths="reference": the reference's refined depths are injected too (the fine pass runs at its depths);
+      depths="own": this build's refinement, whose depths must equal the reference's refinement (oracle) of OUR
+      coarse weights (<= 2e-5), the coarse weights the reference's (<= 1e-5).
+    * Both MLPs' gradients equal the reference's algorithm (the oracle, pinned to the reference's gradients at 1.6e-5
+      under the reference's ReLU decisions: test_oracle_golden) evaluated under the ReLU decisions the HIP forward took
+      (read back from its saved activations) -- strict, every element.
+    * Those decisions equal the reference's own (recorded in the golden) except at fp32 ties: units whose
+      pre-activation is within TIE_REL of zero, where two correct fp32 evaluations may land on either side of the
+      kink (the oracle itself has 10 such units against the reference on this step). Counted and reported.
+    * The direct difference to the reference's gradients (which includes the ties' contributions) is reported and
+      held to the end-to-end gate."""
     from yanerf_amd import ops
     g = golden("train_step_lego")
     R = int(g["n_rays"])
     tr = make_trainer(precision, g["seeds"], n_rays=R)
     img = torch.zeros(1, 800, 800, 3, device=DEV)
     img.view(1, -1, 3)[0, torch.as_tensor(g["pixel_ids"][0], device=DEV)] = t(g["gt_rgb"])
-    with ops.injected_randomness(pixel_ids=t(g["pixel_ids"], torch.int64), jitter_u=t(g["jitter_u"]),
-                                 noise=[t(g["noise_coarse"]), t(g["noise_fine"])], pdf_u=t(g["pdf_u"])):
+    draws = dict(pixel_ids=t(g["pixel_ids"], torch.int64), jitter_u=t(g["jitter_u"]),
+                 noise=[t(g["noise_coarse"]), t(g["noise_fine"])], pdf_u=t(g["pdf_u"]))
+    if depths == "reference":
+        draws["z_fine"] = t(g["z_fine"])
+    with ops.injected_randomness(**draws):
         out = tr.step(t(g["pose"]), t(g["focal"]), img)
     torch.cuda.synchronize()
     # the injected pixel ids were used (the gathered targets are the golden's)
@@ -77,25 +103,49 @@ def test_trainer_step_matches_reference_step(golden, precision):
     np.testing.assert_allclose(float(obj), float(g["objective"][0]), atol=1e-6, rtol=1e-5)
     np.testing.assert_allclose(float(out["sq_coarse"].sum() / (R * 3)), float(g["loss_prev_stage_rgb_mse"][0]),
                                atol=1e-7, rtol=1e-5)
-    worst = 0.0
-    for i, m in enumerate(tr.models):
-        for name, p in m.named_parameters():
-            v = n(p.grad).astype(np.float64)
-            if f"grad{i}:{name}" in g:
-                ref = g[f"grad{i}:{name}"].astype(np.float64)
-                mx = np.abs(ref).max()
-                close_frac(v, ref, 5e-3 * mx, 0.98, 3e-2 * mx)
-                rel = np.linalg.norm(v - ref) / max(np.linalg.norm(ref), 1e-30)
-            else:
-                s, nn = g[f"gradsum{i}:{name}"]
-                np.testing.assert_allclose(np.linalg.norm(v), nn, rtol=1e-3)
-                idx, ref = g[f"gradidx{i}:{name}"], g[f"gradval{i}:{name}"].astype(np.float64)
-                mx = np.abs(ref).max()
-                close_frac(v.reshape(-1)[idx], ref, 5e-3 * mx, 0.98, 3e-2 * mx)
-                rel = np.linalg.norm(v.reshape(-1)[idx] - ref) / max(np.linalg.norm(ref), 1e-30)
-            worst = max(worst, rel)
-    print(f"{precision}: trainer step vs reference, worst per-tensor relative L2 of the gradients {worst:.2e}")
-    assert worst < 2e-2
+    w_err = float(np.abs(n(tr.passes[0].w) - g["coarse_weights"]).max())
+    assert w_err <= 1e-5, w_err
+    z_ours = n(tr.zf)
+    report = dict(precision=precision, depths=depths, coarse_weights_max_err=w_err,
+                  rays_with_other_depths=int((np.abs(z_ours - g["z_fine"]).max(-1) > 2e-5).sum()))
+    if depths == "own":
+        z_or = O.refine(n(tr.zc), n(tr.passes[0].w), 128, random_sampling=True, u=g["pdf_u"].reshape(R, 128))
+        report["max_depth_err_vs_oracle_refine_of_our_weights"] = float(np.abs(z_ours - z_or).max())
+        assert report["max_depth_err_vs_oracle_refine_of_our_weights"] <= 2e-5, report
+    masks = [hip_relu_masks(tr.passes[k].saved, R * tr.passes[k].P) for k in range(2)]
+    pc, pf = (make_nerf_mlp_params(LEGO_ARCH, int(s)) for s in g["seeds"])
+    ora = O.train_step_grads(pc, pf, O.MLPArch.from_dict(LEGO_ARCH), LEGO_TRAIN_CFG, *lego_oracle_inputs(g),
+                             z_fine=z_ours, relu_masks=tuple(masks))
+    strict = {0: 0.0, 1: 0.0}
+    for i, key in ((0, "grads_coarse"), (1, "grads_fine")):
+        for name, p in tr.models[i].named_parameters():
+            e = grad_err(n(p.grad), ora[key][name])
+            strict[i] = max(strict[i], e)
+            assert e <= STRICT_GRAD, (i, name, e)
+    # the HIP decisions vs the reference's (coarse always; fine at the reference's depths) or, on the fine pass at our
+    # own depths, vs the oracle's own signs there (the reference's algorithm at those depths)
+    ties = {}
+    for k, cache in ((0, ora["render"]["cache_c"]), (1, ora["render"]["cache_f"])):
+        if k == 0 or depths == "reference":
+            other = golden_relu_masks(g, k)
+        else:
+            other = dict(trunk=[zz > 0 for zz in cache.layer_pre], color=cache.c0_pre > 0)
+        ties[k] = relu_ties(masks[k], other, cache)
+        assert ties[k][1] <= TIE_REL, (k, ties[k])
+    direct = {0: 0.0, 1: 0.0}
+    loose_rel = 0.0
+    for i, name, v, ref, norms in golden_grad_pairs(g, tr.models):
+        direct[i] = max(direct[i], grad_err(v, ref))
+        loose_rel = max(loose_rel, loose_grad_gate(v, ref, name))
+    report.update(coarse_grad_max_rel_err_vs_oracle_same_relu=strict[0],
+                  fine_grad_max_rel_err_vs_oracle_same_relu=strict[1],
+                  relu_ties_coarse=ties[0][0], relu_ties_fine=ties[1][0],
+                  relu_tie_max_rel_preact=max(ties[0][1], ties[1][1]),
+                  coarse_grad_max_rel_err_vs_reference=direct[0], fine_grad_max_rel_err_vs_reference=direct[1],
+                  grad_worst_rel_l2_vs_reference=loose_rel)
+    print(f"trainer step vs reference: {report}")
+    write_report("train_step", f"lego {precision} depths={depths}", report)
+    assert loose_rel < 2e-2
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
@@ -283,7 +333,7 @@ def test_trainer_render_matches_reference_render(golden):
         fine_at = oracle_fine_at(O, make_nerf_mlp_params(LEGO_ARCH, int(g["seeds"][1])),
                                  O.MLPArch.from_dict(LEGO_ARCH), o_r, d_r, O.RaymarchOpts(background_density_bias=1e-6))
         split_gate(n(f), g["fine_features"], z_gpu, z_ref, n(d), g["fine_depths"], fine_at=fine_at,
-                   tag=f"render_eval {precision}")
+                   tag=f"render_eval {precision}", coarse=(O, n(zc), n(rb_w), 128))
 
 
 def tr_coarse_weights(tr, g, H, W):
@@ -352,4 +402,5 @@ def test_full_image_800_vs_oracle(precision):
     z_gpu = n(ops.refine(t(z), ro.prev_stage.aux["weights"].reshape(S, 64), 128, det=True))
     fine_at = oracle_fine_at(O, pf, O.MLPArch.from_dict(LEGO_ARCH), o, dd, O.RaymarchOpts(background_density_bias=1e-6))
     split_gate(n(f).reshape(-1, 3)[idx], ref["fine"][0], z_gpu, ref["z_fine"], n(d).reshape(-1)[idx],
-               ref["fine"][1].reshape(-1), fine_at=fine_at, tag=f"800x800 {precision}")
+               ref["fine"][1].reshape(-1), fine_at=fine_at, tag=f"800x800 {precision}",
+               coarse=(O, z, n(ro.prev_stage.aux["weights"]), 128))

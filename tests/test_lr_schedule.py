@@ -1,6 +1,8 @@
 """The reference runner's learning-rate schedule (runners/utils.py:65-109 applied per iteration by runners/apis.py:66-68,
 linear world-size scaling of scripts/run.py:152-156), against golden values produced by the reference's own functions
 (tests/golden/make_golden.py: gen_lr_schedule). CPU only."""
+import ast
+
 import numpy as np
 import pytest
 import torch
@@ -80,3 +82,37 @@ def test_trainer_optimizer_state_resumes_under_reference_scheduler():
     sched = create_lr_scheduler(opt, r)
     apply_schedule(opt, sched, r, 2000)
     assert opt.param_groups[0]["lr"] == lr_at(r, 2000)
+
+
+ITER_CASES = ["lego_w1", "lego_w8", "lego_w3", "lego_cos_w2_b2", "fern_w1", "fern_w4", "fern_w8"]
+
+
+@pytest.mark.parametrize("tag", ITER_CASES)
+def test_setup_iter_based_runner_matches_reference(golden, tag):
+    """scripts/run.py:243-271 run by the reference on its product configs (tests/golden/make_golden.py:
+    gen_iter_runner): the training loader's length, every rescaled '*iters' / epoch key (including the reference's own
+    rescale of num_iters_on_one_gpu, which lands one above num_iters for Fern at 8 ranks), and the per-iteration
+    learning rate of the rescaled, world-scaled schedule -- all bit-equal."""
+    from yanerf_amd.lr_schedule import setup_iter_based_runner, train_loader_len
+    g = golden("iter_runner")
+    cfgfile, over, n_train, world, bs = (str(x) for x in g[f"{tag}:case"])
+    n_train, world, bs = int(n_train), int(world), int(bs)
+    runner = dict(Config.fromfile(str(yanerf_boot.PKG_DIR / cfgfile)).runner)
+    runner.update(ast.literal_eval(over))  # the case's overrides (a dict literal written by the generator)
+    n_loader = train_loader_len(n_train, world, bs)
+    assert n_loader == int(g[f"{tag}:len_loader"])
+    r = setup_iter_based_runner(runner, n_loader, world, bs)
+    got = np.array([float(r[k]) for k in g["keys"]])
+    np.testing.assert_array_equal(got, g[f"{tag}:values"])
+    lrs = np.array([lr_at(r, int(it), world) for it in g["iters"]])
+    np.testing.assert_array_equal(lrs, g[f"{tag}:lr"])
+
+
+def test_lr_at_uses_restored_init_lr():
+    """A resumed optimizer's param_group['init_lr'] drives the reference's schedulers (min_lr stays the config's)."""
+    r = _runner({})
+    opt = torch.optim.Adam([{"params": [torch.nn.Parameter(torch.zeros(1))], "init_lr": 7e-4}], lr=7e-4)
+    sched = create_lr_scheduler(opt, r)
+    for it in (0, 500, 1000, 1001, 5000, 123456):
+        apply_schedule(opt, sched, r, it)
+        assert lr_at(r, it, 1, init_lr=7e-4) == opt.param_groups[0]["lr"]

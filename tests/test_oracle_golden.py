@@ -186,3 +186,32 @@ def test_conditional_mlp(golden):
                                          code=g["codes"][b].reshape(-1))
         np.testing.assert_allclose(sig, g["sigma"][b], atol=2e-5, rtol=1e-5)
         np.testing.assert_allclose(rgb, g["rgb"][b], atol=2e-6)
+
+
+def test_train_step_lego_strict_under_reference_relu_decisions(golden):
+    """The oracle's training step at the reference's refined depths and under the reference's own ReLU decisions
+    (both recorded in the golden): every gradient element of both MLPs within 1e-4 * max of the reference's (measured
+    7.5e-6 coarse, 1.6e-5 fine). Where the oracle's own signs differ from the reference's, the pre-activation is an fp32
+    tie (parity_gates.relu_ties; measured: 10 units, all within 6e-6 of zero relative to their layer)."""
+    from parity_gates import STRICT_GRAD, TIE_REL, golden_relu_masks, grad_err, relu_ties
+    g = golden("train_step_lego")
+    arch = O.MLPArch.from_dict(LEGO_ARCH)
+    pc, pf = (make_nerf_mlp_params(LEGO_ARCH, int(s)) for s in g["seeds"])
+    o, d, t, xy = O.sample_rays_train(g["pose"], g["focal"], 800, 800, 2.0, 6.0, 64, g["pixel_ids"], g["jitter_u"])
+    R = int(g["n_rays"])
+    masks = (golden_relu_masks(g, 0), golden_relu_masks(g, 1))
+    res = O.train_step_grads(pc, pf, arch, _lego_cfg(0.2), o.reshape(R, 3), d.reshape(R, 3), t.reshape(R, 64),
+                             g["gt_rgb"], (g["noise_coarse"] * np.float32(0.2)).astype(np.float32),
+                             (g["noise_fine"] * np.float32(0.2)).astype(np.float32), g["pdf_u"], z_fine=g["z_fine"],
+                             relu_masks=masks)
+    for i, key in ((0, "grads_coarse"), (1, "grads_fine")):
+        for k, v in res[key].items():
+            if f"grad{i}:{k}" in g:
+                e = grad_err(v, g[f"grad{i}:{k}"])
+            else:
+                e = grad_err(v.reshape(-1)[g[f"gradidx{i}:{k}"]], g[f"gradval{i}:{k}"])
+            assert e <= STRICT_GRAD, (i, k, e)
+    for k, cache in ((0, res["render"]["cache_c"]), (1, res["render"]["cache_f"])):
+        own = dict(trunk=[z > 0 for z in cache.layer_pre], color=cache.c0_pre > 0)
+        n_ties, worst = relu_ties(own, masks[k], cache)
+        assert worst <= TIE_REL, (k, n_ties, worst)

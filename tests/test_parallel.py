@@ -114,3 +114,33 @@ def test_eval_order_matches_distributed_sampler():
             for rank in range(world):
                 ref = list(DistributedSampler(range(n), num_replicas=world, rank=rank, shuffle=False))
                 assert parallel.eval_order(n, rank, world) == ref
+
+
+def _run_bench_dist(extra, nproc=2, timeout=300, env=None):
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(root / "bench.py"),
+           "--gpus", str(nproc)] + extra
+    e = dict(os.environ, **(env or {}))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]  # rank 0 prints ONE JSON line
+    return json.loads(lines[0])
+
+
+def test_bench_distributed_fields_gloo_world2():
+    """bench.py under torch.distributed.run with two CPU ranks over gloo (--dist-selftest: the N-rank plumbing, no
+    GPU work): the line carries the backend and world size the process group reports, every rank's ms/step and the
+    exposed exchange time, and the two-bucket exchange averages the ranks' gradients."""
+    d = _run_bench_dist(["--steps", "3", "--dist-selftest"])
+    info = d["distributed"]
+    assert d["n_gpus"] == 2 and info["backend"] == "gloo" and info["world_size"] == 2
+    assert len(info["ms_per_step_per_rank"]) == 2 and info["ms_per_step_min"] <= info["ms_per_step_max"]
+    assert len(info["allreduce_exposed_ms_per_rank"]) == 2 and info["allreduce_exposed_ms_max"] >= 0
+    assert info["grad_exchange"] == "bucketed" and info["grad_bytes"] == 4 * 1_191_688
+    assert info["selftest_grad_ok"]

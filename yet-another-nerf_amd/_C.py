@@ -6,11 +6,24 @@ the ops raises immediately (there is no CPU or torch fallback).
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 from ctypes import POINTER, Structure, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_uint32, c_uint64, c_void_p
 from pathlib import Path
 
-LIB_PATH = Path(os.environ.get("YANERF_HIP_LIB", Path(__file__).resolve().parent / "libyanerf_hip.so"))
+PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("YANERF_HIP_LIB", PKG / "libyanerf_hip.so"))
+# the files the library's build id hashes, in the Makefile's order (csrc/Makefile: SRC_SHA)
+SOURCES = [PKG / "csrc" / f for f in ("render.hip", "mlp.hip", "common.hpp")] + [
+    PKG.parent / "include" / "yanerf_hip.h", PKG / "csrc" / "Makefile"]
+
+
+def source_id() -> str:
+    """SHA-256 prefix of the HIP sources in this tree (what a library built from them reports as its build id)."""
+    h = hashlib.sha256()
+    for f in SOURCES:
+        h.update(f.read_bytes())
+    return h.hexdigest()[:16]
 
 PREC_F32 = 0
 PREC_BF16 = 1
@@ -18,7 +31,8 @@ PREC_F32X3 = 2  # fp32 as three bf16 terms, six bf16 MFMAs per product (include/
 
 # every symbol include/yanerf_hip.h declares (checked by tests/test_capi.py)
 EXPORTS = (
-    "yanerf_last_error", "yanerf_version", "yanerf_raygen", "yanerf_mlp_num_params", "yanerf_mlp_packed_bytes",
+    "yanerf_last_error", "yanerf_version", "yanerf_build_id", "yanerf_raygen", "yanerf_mlp_num_params",
+    "yanerf_mlp_packed_bytes",
     "yanerf_mlp_pack", "yanerf_mlp_saved_bytes", "yanerf_mlp_bwd_workspace_bytes", "yanerf_mlp_forward",
     "yanerf_mlp_backward", "yanerf_mlp_backward_phase", "yanerf_composite_forward", "yanerf_composite_backward",
     "yanerf_composite_train", "yanerf_sample_pdf",
@@ -39,7 +53,7 @@ class RaymarchOpts(Structure):
         ("capping", c_int32), ("weight_fn", c_int32), ("blend_output", c_int32), ("hard_background", c_int32),
         ("density_relu", c_int32), ("background_opacity", c_float), ("background_density_bias", c_float),
         ("bg_default", c_float * 4), ("bg_default_n", c_int32), ("noise_mode", c_int32), ("noise_std", c_float),
-        ("seed", c_uint64), ("offset", c_uint64),
+        ("seed", c_uint64), ("offset", c_uint64), ("rng_base", c_void_p),
     ]
 
 
@@ -66,8 +80,9 @@ def lib():
     sig = {
         "yanerf_last_error": (c_char_p, []),
         "yanerf_version": (c_int, []),
+        "yanerf_build_id": (c_char_p, []),
         "yanerf_raygen": (c_int, [P, P, P, P, i64, i64, i64, i64, c_float, c_float, c_float, c_float, i64, c_int, P,
-                                  c_uint64, c_uint64, P, P, P, P, P, P]),
+                                  c_uint64, c_uint64, P, P, P, P, P, P, P, P]),
         "yanerf_mlp_num_params": (c_int, [POINTER(MlpDesc)]),
         "yanerf_mlp_packed_bytes": (i64, [POINTER(MlpDesc), c_int]),
         "yanerf_mlp_pack": (c_int, [POINTER(MlpDesc), c_int, P, P, P]),
@@ -82,7 +97,7 @@ def lib():
         "yanerf_composite_train": (c_int, [POINTER(RaymarchOpts), P, P, P, P, P, P, P, P, i64, i64, i64, i64, i64,
                                            i64, c_float, P, P, P, P, P, P, P, P, P]),
         "yanerf_sample_pdf": (c_int, [P, P, i64, i64, i64, c_int, P, c_uint64, c_uint64, P, P]),
-        "yanerf_refine": (c_int, [P, P, i64, i64, i64, c_int, P, c_uint64, c_uint64, c_int, P, P]),
+        "yanerf_refine": (c_int, [P, P, i64, i64, i64, c_int, P, c_uint64, c_uint64, c_int, P, P, P]),
         "yanerf_rgb_loss": (c_int, [P, P, P, i64, i64, i64, i64, i64, c_float, P, P, P]),
         "yanerf_adam": (c_int, [P, P, P, P, i64, c_double, c_double, c_double, c_double, c_double, i64, P]),
     }
@@ -90,6 +105,11 @@ def lib():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    if "YANERF_HIP_LIB" not in os.environ:  # an explicitly chosen library (A/B builds) is taken as given
+        built, src = L.yanerf_build_id().decode(), source_id()
+        if built != src:
+            raise HipError(f"{LIB_PATH} was built from other sources (build id {built}, sources {src}): rebuild it with "
+                           f"`python -c \"import __graft_entry__ as g; g.build()\"`")
     _lib = L
     return L
 

@@ -56,7 +56,13 @@ __global__ void raygen_kernel(const float* __restrict__ poses, const float* __re
                               float far, int64_t P, int jitter_mode, const float* __restrict__ jitter_u,
                               uint64_t seed, uint64_t offset, float* __restrict__ origins,
                               float* __restrict__ directions, float* __restrict__ lengths,
-                              float* __restrict__ xys, int64_t* __restrict__ ids_out) {
+                              float* __restrict__ xys, int64_t* __restrict__ ids_out,
+                              const float* __restrict__ bounds, const uint64_t* __restrict__ rng_base) {
+  if (bounds) {  // device-resident depth range (no host read of LLFF's per-image bounds)
+    near = bounds[0];
+    far = bounds[1];
+  }
+  if (rng_base) offset += *rng_base;  // graph replay: the step's Philox base lives on the device
   const int64_t G = (P + RG_J - 1) / RG_J;  // depth groups per ray (>= 1: the ray-level work needs group 0)
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= B * R * (G > 0 ? G : 1)) return;
@@ -146,7 +152,7 @@ __device__ __forceinline__ float noise_at(const yanerf_raymarch_opts& o, const f
   if (o.noise_mode == 1) {
     n = noise[idx];
   } else {
-    u4 r = philox(o.seed, o.offset, (uint64_t)(idx >> 1));
+    u4 r = philox(o.seed, o.offset + (o.rng_base ? *o.rng_base : 0ull), (uint64_t)(idx >> 1));
     n = (idx & 1) ? normal_from(r.z, r.w) : normal_from(r.x, r.y);
   }
   return n * o.noise_std;
@@ -587,7 +593,8 @@ __device__ __forceinline__ void sort_lds_row(float* row, int n, int lane) {
 __global__ void __launch_bounds__(64) refine_kernel(const float* __restrict__ z, const float* __restrict__ w, int64_t R,
                                                     int P, int NF, int det, const float* __restrict__ u,
                                                     uint64_t seed, uint64_t offset, int add_input,
-                                                    float* __restrict__ out) {
+                                                    float* __restrict__ out, const uint64_t* __restrict__ rng_base) {
+  if (rng_base) offset += *rng_base;
   __shared__ float s_w[kPdfMaxBins], s_cdf[kPdfMaxBins + 1], s_bins[kPdfMaxBins + 1];
   __shared__ float s_mid[kPdfMaxBins + 1];
   __shared__ float s_all[kMergeMax];
@@ -717,11 +724,16 @@ extern "C" {
 
 const char* yanerf_last_error(void) { return g_last_error.c_str(); }
 int yanerf_version(void) { return 1; }
+#ifndef YANERF_SRC_SHA
+#define YANERF_SRC_SHA "unknown"
+#endif
+const char* yanerf_build_id(void) { return YANERF_SRC_SHA; }
 
 int yanerf_raygen(const float* poses, const float* focal, const float* xy, const int64_t* pixel_ids, int64_t B,
                   int64_t R, int64_t grid_w, int64_t grid_h, float cfg_w, float cfg_h, float near, float far,
                   int64_t P, int jitter_mode, const float* jitter_u, uint64_t seed, uint64_t offset, float* origins,
-                  float* directions, float* lengths, float* xys, int64_t* ids_out, void* stream) {
+                  float* directions, float* lengths, float* xys, int64_t* ids_out, const float* bounds,
+                  const uint64_t* rng_base, void* stream) {
   YN_CHECK(poses && focal && origins && directions && xys && (lengths || P == 0), "yanerf_raygen: null pointer");
   YN_CHECK(B >= 0 && R >= 0 && P >= 0, "yanerf_raygen: negative size");
   YN_CHECK(jitter_mode >= 0 && jitter_mode <= 2, "yanerf_raygen: bad jitter_mode %d", jitter_mode);
@@ -733,7 +745,7 @@ int yanerf_raygen(const float* poses, const float* focal, const float* xy, const
   const int64_t nt = n * ((P + RG_J - 1) / RG_J > 0 ? (P + RG_J - 1) / RG_J : 1);
   hipLaunchKernelGGL(raygen_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, as_stream(stream), poses, focal, xy,
                      pixel_ids, B, R, grid_w, grid_h, cfg_w, cfg_h, near, far, P, jitter_mode, jitter_u, seed, offset,
-                     origins, directions, lengths, xys, ids_out);
+                     origins, directions, lengths, xys, ids_out, bounds, rng_base);
   YN_LAUNCH_CHECK("raygen");
   return 0;
 }
@@ -754,7 +766,7 @@ int yanerf_composite_forward(const yanerf_raymarch_opts* o, const float* sigma_r
                              int64_t R, int64_t P, int64_t C, float* features, float* depths, float* alpha,
                              float* weights, void* stream) {
   if (composite_common(o, R, P, C)) return 1;
-  YN_CHECK(o->noise_mode != 1 || noise, "composite: noise_mode 1 needs noise");
+  YN_CHECK(o->noise_mode != 1 || noise, "composite_forward: noise_mode 1 needs noise");
   if (R == 0) return 0;
   hipLaunchKernelGGL(composite_kernel<0>, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, as_stream(stream), *o,
                      sigma_raw, rgb, lengths, directions, bg, noise, R, P, C, features, depths, alpha, weights, nullptr,
@@ -769,6 +781,7 @@ int yanerf_composite_backward(const yanerf_raymarch_opts* o, const float* sigma_
                               int64_t P, int64_t C, float* g_sigma, float* g_rgb, void* stream) {
   if (composite_common(o, R, P, C)) return 1;
   YN_CHECK(g_features && g_sigma && g_rgb, "composite_backward: null gradient pointer");
+  YN_CHECK(o->noise_mode != 1 || noise, "composite_backward: noise_mode 1 needs noise");
   if (R == 0) return 0;
   hipLaunchKernelGGL(composite_kernel<1>, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, as_stream(stream), *o,
                      sigma_raw, rgb, lengths, directions, bg, noise, R, P, C, nullptr, nullptr, nullptr, nullptr,
@@ -787,6 +800,7 @@ int yanerf_composite_train(const yanerf_raymarch_opts* o, const float* sigma_raw
   if (composite_common(o, R, P, C)) return 1;
   YN_CHECK(features && depths && alpha && weights && g_sigma && g_rgb && image && xys,
            "composite_train: null pointer");
+  YN_CHECK(o->noise_mode != 1 || noise, "composite_train: noise_mode 1 needs noise");
   YN_CHECK(H > 0 && W > 0, "composite_train: image size %lld x %lld", (long long)H, (long long)W);
   if (R == 0) return 0;
   const CompositeLoss loss{image, xys, R / B, H, W, scale, sq_err_per_ray, g_features};
@@ -809,13 +823,14 @@ int yanerf_sample_pdf(const float* bins, const float* weights, int64_t R, int64_
 }
 
 int yanerf_refine(const float* lengths, const float* ray_weights, int64_t R, int64_t P, int64_t n_fine, int det,
-                  const float* u, uint64_t seed, uint64_t offset, int add_input, float* lengths_out, void* stream) {
+                  const float* u, uint64_t seed, uint64_t offset, int add_input, float* lengths_out,
+                  const uint64_t* rng_base, void* stream) {
   YN_CHECK(P >= 3 && P - 2 <= kPdfMaxBins, "refine: P=%lld out of range", (long long)P);
   YN_CHECK(n_fine >= 1, "refine: n_fine must be >= 1");
   YN_CHECK((add_input ? P + n_fine : n_fine) <= kMergeMax, "refine: P + n_fine > %d", kMergeMax);
   if (R == 0) return 0;
   hipLaunchKernelGGL(refine_kernel, dim3((unsigned)R), dim3(64), 0, as_stream(stream), lengths, ray_weights, R, (int)P,
-                     (int)n_fine, det, u, seed, offset, add_input, lengths_out);
+                     (int)n_fine, det, u, seed, offset, add_input, lengths_out, rng_base);
   YN_LAUNCH_CHECK("refine");
   return 0;
 }

@@ -7,8 +7,12 @@ create_lr_scheduler), applied once per iteration before the forward in runners/a
     if warmup_steps > 0 and passed_iter <= warmup_steps:          # then warm-up (overrides the decay)
         warmup_lr_scheduler(optimizer, passed_iter, warmup_steps, warmup_lr)
 
-`passed_iter` counts from 0 (apis.py:42, 117). With torch.distributed and `linear_scale`, init_lr and min_lr (not
-warmup_lr) are multiplied by the world size before the optimizer is built (scripts/run.py:152-156).
+`passed_iter` counts from 0 (apis.py:42, 117). Before any of that, scripts/run.py:144 converts the iteration-based
+runner config to epochs (`setup_iter_based_runner`, run.py:243-271): num_iters becomes a whole number of epochs of the
+rank's training loader, and every other '*iters' key (lr_decay_iters) is rescaled by the same factor -- at 8 ranks on
+Lego's 100 training images num_iters 200000 -> 25012 and lr_decay_iters 250000 -> 31265. With torch.distributed and
+`linear_scale`, init_lr and min_lr (not warmup_lr) are then multiplied by the world size before the optimizer is built
+(run.py:152-156).
 
 The optimizer-level functions below write `param_group["lr"]` from `param_group["init_lr"]` exactly as the reference
 does, so an optimizer restored from a NeRFTrainer checkpoint (checkpoint.adam_state_from_flat stores `init_lr`) keeps
@@ -67,6 +71,30 @@ def apply_schedule(optimizer, scheduler, runner_cfg, passed_iter: int) -> None:
         warmup_lr_scheduler(optimizer, passed_iter, warm, float(_get(runner_cfg, "warmup_lr")))
 
 
+def train_loader_len(n_train: int, world_size: int = 1, batch_size: int = 1) -> int:
+    """len() of the reference's training DataLoader (runners/utils.py:112-145): a DistributedSampler under
+    torch.distributed (ceil(N / world) samples per rank, padded), batches of batch_size with drop_last=True."""
+    n = math.ceil(n_train / world_size) if world_size > 1 else int(n_train)
+    return n // int(batch_size)
+
+
+def setup_iter_based_runner(runner_cfg, len_loader: int, world_size: int = 1, batch_size: int = 1) -> dict:
+    """scripts/run.py:243-271 on a copy of the runner config (key order kept: the reference rescales the keys in
+    iteration order, and `num_iters_on_one_gpu`, appended by the function itself, is rescaled too -- after the
+    original keys, so the factor they see is the unmodified one)."""
+    r = dict(runner_cfg)
+    iters_per_epoch = int(len_loader) * int(world_size) * int(batch_size)
+    r["num_iters_on_one_gpu"] = r["num_iters"]
+    r["num_epochs"] = math.ceil(r["num_iters"] / iters_per_epoch)
+    r["num_iters"] = r["num_epochs"] * int(len_loader)
+    r["val_per_epoch"] = max(1, math.floor(r["val_per_iter"] / iters_per_epoch))
+    r["save_per_epoch"] = max(1, math.floor(r["save_per_iter"] / iters_per_epoch))
+    for key in list(r.keys()):
+        if key != "num_iters" and "iters" in key:
+            r[key] = math.ceil(r[key] * (r["num_iters"] / r["num_iters_on_one_gpu"]))
+    return r
+
+
 def scaled_lrs(runner_cfg, world_size: int = 1):
     """(init_lr, min_lr) after the linear world-size scaling of scripts/run.py:152-156 (only under
     torch.distributed, i.e. world_size > 1, and only when runner.linear_scale is set)."""
@@ -76,10 +104,14 @@ def scaled_lrs(runner_cfg, world_size: int = 1):
     return init, mn
 
 
-def lr_at(runner_cfg, it: int, world_size: int = 1) -> float:
+def lr_at(runner_cfg, it: int, world_size: int = 1, init_lr=None) -> float:
     """The learning rate the reference runner uses at iteration `it` (0-based), as a pure function: the decay
-    schedule from init_lr, then the warm-up override while it <= warmup_steps (warmup_steps > 0)."""
+    schedule from init_lr, then the warm-up override while it <= warmup_steps (warmup_steps > 0). `runner_cfg` is the
+    config after setup_iter_based_runner. `init_lr` overrides the (world-scaled) config value, as a resumed
+    optimizer's param_group["init_lr"] does for the reference's schedulers (run.py:169-178; min_lr stays the config's)."""
     init, mn = scaled_lrs(runner_cfg, world_size)
+    if init_lr is not None:
+        init = float(init_lr)
     kind = _get(runner_cfg, "lr_decay_type")
     decay_iters = _get(runner_cfg, "lr_decay_iters")
     if kind == "exponential":

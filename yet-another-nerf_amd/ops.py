@@ -94,9 +94,12 @@ INJECT = _Injection()
 
 @contextmanager
 def injected_randomness(**queues):
-    """with injected_randomness(pixel_ids=t, jitter_u=t, noise=[nc, nf], pdf_u=t): ...
+    """with injected_randomness(pixel_ids=t, jitter_u=t, noise=[nc, nf], pdf_u=t[, z_fine=t]): ...
     Consumed by the registry ops and by NeRFTrainer.step alike (pixel ids, stratified jitter, the coarse then the
-    fine density noise, the refinement uniforms), in the order the reference draws them."""
+    fine density noise, the refinement uniforms), in the order the reference draws them. `z_fine` (optional) is the
+    reference's refined depths (RayPointRefiner.forward's output, renderers/utils.py:48-69): given, the fine pass runs
+    at exactly those depths instead of this build's refinement, so the fine stage and its gradients can be held to
+    strict gates independent of sample_pdf's ill-conditioned branch (tests/parity_gates.py)."""
     INJECT.queues = {k: list(v) if isinstance(v, (list, tuple)) else [v] for k, v in queues.items()}
     try:
         yield
@@ -105,12 +108,28 @@ def injected_randomness(**queues):
 
 
 # ----------------------------------------------------------------------------------------- ray generation
-def raygen(poses: torch.Tensor, focal: torch.Tensor, *, n_pts: int, near: float, far: float, cfg_w: int, cfg_h: int,
+def depth_bounds(near, far, dev):
+    """(near, far, bounds): floats pass through; tensor bounds collapse to their means (ray_sampler.py:280-283:
+    `.mean().item()`). Host tensors are averaged on the host; device tensors are averaged ON the device into
+    `bounds` [2] (the kernel reads them there), so a step fed device-resident LLFF bounds never syncs the host."""
+    def dev_mean(x):
+        return isinstance(x, torch.Tensor) and x.device.type != "cpu"
+
+    if dev_mean(near) or dev_mean(far):
+        vals = [x.float().mean().reshape(1) if isinstance(x, torch.Tensor) else torch.tensor([float(x)])
+                for x in (near, far)]
+        return 0.0, 0.0, torch.cat([v.to(dev, non_blocking=True) for v in vals]).contiguous()
+    near = near.float().mean().item() if isinstance(near, torch.Tensor) else float(near)
+    far = far.float().mean().item() if isinstance(far, torch.Tensor) else float(far)
+    return near, far, None
+
+
+def raygen(poses: torch.Tensor, focal: torch.Tensor, *, n_pts: int, near, far, cfg_w: int, cfg_h: int,
            xy: Optional[torch.Tensor] = None, pixel_ids: Optional[torch.Tensor] = None, n_rays: Optional[int] = None,
            grid_hw: Optional[Tuple[int, int]] = None, jitter: Optional[object] = None):
     """_xy_to_ray_bundle (ray_sampler.py:249-314) on the GPU. Pixel source: `xy` [B,R,2] float, `pixel_ids`
     [B,R] int64 into grid_hw, or neither (uniform sampling without replacement of n_rays pixels).
-    jitter: None, "philox", or a [B,R,P] tensor of injected uniforms.
+    jitter: None, "philox", or a [B,R,P] tensor of injected uniforms. near / far: floats or tensors (depth_bounds).
     Returns origins [B,R,3], directions [B,R,3], lengths [B,R,P], xys [B,R,2], ids [B,R] (or None)."""
     _dev(poses, focal, xy, pixel_ids)
     B = poses.shape[0]
@@ -138,10 +157,11 @@ def raygen(poses: torch.Tensor, focal: torch.Tensor, *, n_pts: int, near: float,
         mode, ju = 1, _f32c(jitter.reshape(B, R, n_pts))
     else:
         mode, ju = 2, None
+    near, far, bounds = depth_bounds(near, far, dev)
     seed, off = RNG.next(B * R * n_pts)
     _C.check(_C.lib().yanerf_raygen(_p(poses), _p(focal), _p(xy), _p(pixel_ids), B, R, gw, gh, float(cfg_w),
                                     float(cfg_h), float(near), float(far), n_pts, mode, _p(ju), seed, off, _p(o), _p(d),
-                                    _p(z), _p(xys), _p(ids), _stream()), "yanerf_raygen")
+                                    _p(z), _p(xys), _p(ids), _p(bounds), None, _stream()), "yanerf_raygen")
     return o, d, z, xys, ids
 
 
@@ -370,7 +390,7 @@ def refine(lengths: torch.Tensor, ray_weights: torch.Tensor, n_fine: int, det: b
     out = torch.empty(R, tot, dtype=_F32, device=z.device)
     seed, off = RNG.next(R * n_fine)
     _C.check(_C.lib().yanerf_refine(_p(z), _p(w), R, P, n_fine, int(det), _p(uu), seed, off, int(add_input), _p(out),
-                                    _stream()), "yanerf_refine")
+                                    None, _stream()), "yanerf_refine")
     return out.view(*lengths.shape[:-1], tot)
 
 

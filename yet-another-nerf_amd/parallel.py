@@ -2,9 +2,12 @@
 
 Reference: DDP over NCCL (scripts/run.py:162-166; runners/utils.py:216-238), one image / 4096 rays per rank
 per step, gradient all-reduce (average) every step and an all_gather of per-image metrics in evaluation
-(apis.py:173-177). Here the two MLPs' 1,191,688 fp32 gradients live in ONE flat buffer, so a step issues a
-single all-reduce of 4.77 MB (one bucket, well under the point where xGMI ring bandwidth matters: ~55 us on one
-153 GB/s link at 8 ranks) instead of DDP's hook-driven per-bucket calls.
+(apis.py:173-177). Here the two MLPs' 1,191,688 fp32 gradients live in ONE flat buffer, and NeRFTrainer.step
+exchanges it in two buckets, one per model (2.38 MB each): the coarse bucket's all-reduce is started asynchronously
+right after the coarse MLP backward and runs on the collective stream while the fine MLP backward computes; only the
+fine bucket's all-reduce is exposed (~55 us for all 4.77 MB on one 153 GB/s xGMI link at 8 ranks by a ring estimate).
+`grad_exchange="single"` (or YANERF_GRAD_EXCHANGE=single) is the one-call fallback: both backwards, then one
+all-reduce of the whole buffer. The per-element sums are the same either way.
 """
 from __future__ import annotations
 
@@ -104,6 +107,16 @@ def max_over_ranks(value: float, device=None) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def allgather_floats(value: float, device=None) -> List[float]:
+    """Every rank's `value`, in rank order (one all_gather of a float64; [value] without a process group)."""
+    if not is_dist():
+        return [float(value)]
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    _all_gather(parts, t)
+    return [float(x.item()) for x in parts]
 
 
 def barrier() -> None:

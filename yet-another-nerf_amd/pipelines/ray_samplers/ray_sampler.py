@@ -98,10 +98,7 @@ class RaySampler(torch.nn.Module):
         # ray_sampler.py:280-283: tensor bounds collapse to their mean (LLFF per-image near/far)
         near = min_depth if min_depth is not None else self._min_depth
         far = max_depth if max_depth is not None else self._max_depth
-        if isinstance(near, torch.Tensor):
-            near = near.mean().item()
-        if isinstance(far, torch.Tensor):
-            far = far.mean().item()
+        # (ops.depth_bounds: device tensors are averaged on the device and read by the kernel -- no host sync)
         jitter = None
         if cfg["stratified"]:
             inj = ops.INJECT.take("jitter_u")

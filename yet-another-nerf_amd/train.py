@@ -13,12 +13,13 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
 
 from . import _C, ops, parallel
-from .lr_schedule import lr_at, scaled_lrs  # noqa: F401  (lr_at re-exported: train.lr_at)
+from .lr_schedule import lr_at, scaled_lrs, setup_iter_based_runner, train_loader_len  # noqa: F401
 from .pipelines.models import MODELS
 
 F32 = torch.float32
@@ -55,12 +56,22 @@ def _p(t):
 class NeRFTrainer:
     def __init__(self, pipeline_cfg, *, precision: str = "fp32", device="cuda", lr: Optional[float] = None,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: Optional[float] = None, seed: int = 42,
-                 n_rays: Optional[int] = None, overlap: Optional[bool] = None, runner_cfg=None):
+                 n_rays: Optional[int] = None, overlap: Optional[bool] = None, runner_cfg=None,
+                 train_set_size: Optional[int] = None, batch_size: int = 1, grad_exchange: Optional[str] = None):
         """pipeline_cfg: the `pipeline:` section of a reference config (lego.yml / fern.yml).
         runner_cfg: its `runner:` section. When given, every step uses the reference schedule
         (lr_schedule.lr_at: decay, then warm-up; init_lr / min_lr linearly scaled by the world size under
         torch.distributed, scripts/run.py:152-156) and its weight_decay; `lr` then must be None. Without it the
         learning rate is the constant `lr` (default 5e-4).
+        train_set_size: the number of training images (Lego 100, Fern 17). Given with runner_cfg, the config is first
+        converted as scripts/run.py:144 does (lr_schedule.setup_iter_based_runner over the rank's training loader of
+        that many images at this world size and `batch_size`): num_iters and lr_decay_iters are rescaled, which at
+        world > 1 changes the schedule. Without it the runner config is used as written (exact at world 1 when the
+        train set divides num_iters).
+        grad_exchange (world > 1 only): "bucketed" (default) = one all-reduce per model, the coarse bucket started
+        right after the coarse MLP backward and overlapped with the fine one (this replaces the `overlap` schedule,
+        which only applies at world 1); "single" = one all-reduce of the whole flat gradient after both backwards
+        (the plain DDP-equivalent fallback). Env YANERF_GRAD_EXCHANGE sets the default. Both give the same sums.
         seed: the weights are initialised from `seed` on every rank (then broadcast from rank 0, as DDP does); the
         trainer's own Philox stream (pixel sampling, jitter, density noise, refinement) is keyed by seed + rank,
         as scripts/run.py:70-71 seeds each rank. torch's global generator is left untouched."""
@@ -99,16 +110,22 @@ class NeRFTrainer:
         self.rng = ops.philox_stream(int(seed) + self.rank)
         self.exp_avg = torch.zeros_like(self.flat.data)
         self.exp_avg_sq = torch.zeros_like(self.flat.data)
-        self.runner_cfg = runner_cfg
         if runner_cfg is not None:
             if lr is not None:
                 raise ValueError("NeRFTrainer: pass either runner_cfg (the reference schedule) or a constant lr")
+            if list(runner_cfg.get("lr_param_groups", None) or []):
+                raise NotImplementedError("NeRFTrainer: runner.lr_param_groups (runners/utils.py:148-184) is not "
+                                          "supported by the fused step (one Adam group); use the registry pipeline")
+            if train_set_size is not None:
+                runner_cfg = setup_iter_based_runner(
+                    runner_cfg, train_loader_len(int(train_set_size), self.world, batch_size), self.world, batch_size)
             # the optimizer's init_lr (param_group["init_lr"], runners/utils.py:148-151), world-scaled
             self.init_lr = scaled_lrs(runner_cfg, self.world)[0]
             wd = runner_cfg.get("weight_decay", 0.0) if weight_decay is None else weight_decay
         else:
             self.init_lr = 5e-4 if lr is None else float(lr)
             wd = 0.0 if weight_decay is None else weight_decay
+        self.runner_cfg = runner_cfg
         self.lr, self.betas, self.eps, self.weight_decay = self.init_lr, betas, eps, float(wd)
         self.step_count = 0
         L = _C.lib()
@@ -135,6 +152,9 @@ class NeRFTrainer:
             overlap = precision == "bf16"
         self.overlap = "both" if overlap is True else overlap
         self.side = torch.cuda.Stream(device=self.dev) if overlap else None
+        self.grad_exchange = grad_exchange or os.environ.get("YANERF_GRAD_EXCHANGE", "bucketed")
+        if self.grad_exchange not in ("bucketed", "single"):
+            raise ValueError(f"NeRFTrainer: grad_exchange {self.grad_exchange!r} (bucketed | single)")
         self.grad_ptrs = [_C.ptr_array([p.grad.data_ptr() for p in ps]) for ps in self.params]
         self.param_ptrs = [_C.ptr_array([p.data_ptr() for p in ps]) for ps in self.params]
         self.events: Optional[Dict[str, List]] = None  # optional per-phase timing probes
@@ -199,10 +219,12 @@ class NeRFTrainer:
                              f"{tuple(focal.shape)})")
 
     def current_lr(self) -> float:
-        """The learning rate of the next step: the reference schedule at passed_iter = steps taken so far."""
+        """The learning rate of the next step: the reference schedule at passed_iter = steps taken so far, from the
+        optimizer's init_lr (the config's, world-scaled, or the one a loaded checkpoint restored: the reference's
+        schedulers read param_group["init_lr"], runners/utils.py:65-86)."""
         if self.runner_cfg is None:
             return self.lr
-        return lr_at(self.runner_cfg, self.step_count, self.world)
+        return lr_at(self.runner_cfg, self.step_count, self.world, init_lr=self.init_lr)
 
     def step(self, pose: torch.Tensor, focal: torch.Tensor, image: torch.Tensor, near=None,
              far=None) -> Dict[str, torch.Tensor]:
@@ -213,11 +235,9 @@ class NeRFTrainer:
         Randomness comes from the trainer's Philox stream, or, inside ops.injected_randomness(...), from the
         injected draws in the reference's order: pixel_ids [1,R] int64, jitter_u [1,R,Pc], noise (coarse [R,Pc],
         then fine [R,Pf]), pdf_u [R,Pn]. The reference's training step is replayed that way by the parity tests."""
-        near = self.near if near is None else (near.float().mean().item() if isinstance(near, torch.Tensor)
-                                               else float(near))
-        far = self.far if far is None else (far.float().mean().item() if isinstance(far, torch.Tensor)
-                                            else float(far))
         self._check_inputs(pose, focal, image)
+        near, far, bounds = ops.depth_bounds(self.near if near is None else near, self.far if far is None else far,
+                                             self.dev)
         L = _C.lib()
         st = ops._stream()
         R = self.R
@@ -240,7 +260,7 @@ class NeRFTrainer:
         jmode = 0 if not self.stratified else (1 if inj_jit is not None else 2)
         _C.check(L.yanerf_raygen(_p(pose), _p(focal), None, _p(inj_ids), 1, R, self.W, self.H, float(self.W),
                                  float(self.H), near, far, self.Pc, jmode, _p(inj_jit), seed, off, _p(self.o),
-                                 _p(self.d), _p(self.zc), _p(self.xys), None, st), "yanerf_raygen")
+                                 _p(self.d), _p(self.zc), _p(self.xys), None, _p(bounds), None, st), "yanerf_raygen")
         scale = 1.0 / (R * C)
         out = {}
         for k, (z, ps) in enumerate(((self.zc, self.passes[0]), (self.zf, self.passes[1]))):
@@ -248,11 +268,15 @@ class NeRFTrainer:
             if k == 1:
                 seed, off = self.rng.next(R * self.Pn)
                 u = ops.INJECT.take("pdf_u") if self.random_refine else None
-                if u is not None:
-                    u = u.to(self.dev, F32).reshape(R, self.Pn).contiguous()
-                _C.check(L.yanerf_refine(_p(self.zc), _p(self.passes[0].w), R, self.Pc, self.Pn,
-                                         0 if self.random_refine else 1, _p(u), seed, off, int(self.append),
-                                         _p(self.zf), st), "yanerf_refine")
+                zi = ops.INJECT.take("z_fine")
+                if zi is not None:  # test mode: the reference's refined depths (ops.injected_randomness)
+                    self.zf.copy_(zi.to(self.dev, F32).reshape(R, self.Pf))
+                else:
+                    if u is not None:
+                        u = u.to(self.dev, F32).reshape(R, self.Pn).contiguous()
+                    _C.check(L.yanerf_refine(_p(self.zc), _p(self.passes[0].w), R, self.Pc, self.Pn,
+                                             0 if self.random_refine else 1, _p(u), seed, off, int(self.append),
+                                             _p(self.zf), None, st), "yanerf_refine")
             P = ps.P
             self._probe(f"mlp_fwd_{k}", lambda: _C.check(L.yanerf_mlp_forward(
                 ctypes.byref(ps.desc), spec.precision, _p(self.packed[k]), _p(self.o), _p(self.d), _p(z), R, P,
@@ -293,18 +317,24 @@ class NeRFTrainer:
                 self.side.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(self.side):
                     self._mlp_backward(0, ctypes.c_void_p(self.side.cuda_stream), self.side)
-        if self.world > 1 and not self.kernel_probes:
+        if self.world > 1 and not self.kernel_probes and self.grad_exchange == "bucketed":
             # Under data parallelism the gradient exchange is split in two buckets, one per model, overlapped with
             # the backward: the coarse MLP's backward runs first, its 2.4 MB all-reduce starts on the
             # collective stream and runs while the fine MLP's backward (the longer one) occupies the GPU; only the
             # fine bucket's all-reduce is exposed before Adam. Per element the result is the same sum over ranks.
+            # Probe "allreduce_exposed": HIP events on the compute stream around the wait, i.e. the time the step
+            # stalls on the exchange after its last backward kernel.
             self._mlp_backward(0, st)
             h = parallel.allreduce_sum_async(self.flat.grad[:self.n_coarse])
             self._mlp_backward(1, st)
             h2 = parallel.allreduce_sum_async(self.flat.grad[self.n_coarse:])
-            parallel.finish_allreduce(h)
-            parallel.finish_allreduce(h2)
+            self._probe("allreduce_exposed", lambda: (parallel.finish_allreduce(h), parallel.finish_allreduce(h2)))
             self.flat.grad.div_(self.world)
+        elif self.world > 1 and not self.kernel_probes:
+            # "single": both backwards, then one all-reduce of the whole flat gradient (all of it exposed)
+            self._mlp_backward(1, st)
+            self._mlp_backward(0, st)
+            self._probe("allreduce_exposed", lambda: parallel.allreduce_mean_(self.flat.grad))
         elif self.kernel_probes:
             # timing probe mode (bench.py's per-kernel roofline): every MLP backward kernel alone on the stream, in the
             # order dX, dW, slab reduce; the result is identical to the other schedules
@@ -333,7 +363,7 @@ class NeRFTrainer:
                 self._mlp_backward(0, ctypes.c_void_p(self.side.cuda_stream), self.side)
             self._mlp_backward(1, st)
             torch.cuda.current_stream().wait_stream(self.side)
-        if self.world == 1 or self.kernel_probes:
+        if self.kernel_probes:
             parallel.allreduce_mean_(self.flat.grad)
         self.lr = self.current_lr()  # the reference schedules before the step (apis.py:66-68)
         self.step_count += 1
@@ -403,7 +433,8 @@ class NeRFTrainer:
             seed, off = self.rng.next(r * self.Pc_eval)
             _C.check(L.yanerf_raygen(_p(pose), _p(focal), None, _p(ids), 1, r, W, H, float(self.W), float(self.H),
                                      near, far, self.Pc_eval, 2 if self.stratified_eval else 0, None, seed, off,
-                                     _p(b["o"]), _p(b["d"]), _p(b["zc"]), _p(b["xys"]), None, st), "yanerf_raygen")
+                                     _p(b["o"]), _p(b["d"]), _p(b["zc"]), _p(b["xys"]), None, None, None, st),
+                     "yanerf_raygen")
             zs = (b["zc"], b["zf"])
             for k in range(2):
                 spec = self.specs[k]
@@ -412,7 +443,7 @@ class NeRFTrainer:
                     seed, off = self.rng.next(r * self.Pn_eval)
                     _C.check(L.yanerf_refine(_p(b["zc"]), _p(b["w"]), r, self.Pc_eval, self.Pn_eval,
                                              0 if self.random_refine_eval else 1, None, seed, off, int(self.append),
-                                             _p(b["zf"]), st), "yanerf_refine")
+                                             _p(b["zf"]), None, st), "yanerf_refine")
                 desc = spec.desc()
                 _C.check(L.yanerf_mlp_forward(ctypes.byref(desc), spec.precision, _p(self.packed[k]), _p(b["o"]),
                                               _p(b["d"]), _p(zs[k]), r, P, _p(b["sigma"]), _p(b["rgb"]), None, st),

@@ -16,10 +16,14 @@ from collections import defaultdict
 def short(name):
     m = re.search(r"yanerf(?:\d+|::)([a-z_0-9]+?)(?:I|E)", name) or re.search(r"([a-z_]+_kernel)", name)
     base = m.group(1) if m else name[:40]
-    if "ItE" in name or "<unsigned short>" in name:
+    if "ItE" in name or "ItLb" in name or "<unsigned short" in name:
         base += "<bf16>"
-    elif "IfE" in name or "<float>" in name:
+    elif "IfE" in name or "IfLb" in name or "<float" in name:
         base += "<f32>"
+    if "Lb1E" in name or ", true>" in name:
+        base += "<train>"
+    elif "Lb0E" in name or ", false>" in name:
+        base += "<infer>"
     return base
 
 

@@ -80,9 +80,15 @@ template <typename T> struct Cfg;
 #ifndef YANERF_F32_WPE
 #define YANERF_F32_WPE 2
 #endif
+// HALVES (forward kernel): 2 = one workgroup holds two independent point tiles (one per 4-wave half, each with its own
+// LDS image) and the second half runs one barrier segment behind the first, so on every SIMD one wave's GEMM runs
+// beside the other's epilogue (the two halves alternate GEMM / epilogue between the shared barriers); 1 = one tile.
+#ifndef YANERF_BF16_PP
+#define YANERF_BF16_PP 1
+#endif
 template <> struct Cfg<float> {
   static constexpr int M = YANERF_F32_M, WAVES = 4, DXWAVES = 4, EPC = 4, KB = 16, APREF = 1, LOWREG = 0,
-                       WPE = YANERF_F32_WPE, PLANES = 1;
+                       WPE = YANERF_F32_WPE, PLANES = 1, HALVES = 1;
   static constexpr bool PM = false;
   typedef float lds_t;
   typedef float st_t;
@@ -90,7 +96,8 @@ template <> struct Cfg<float> {
 };
 template <> struct Cfg<bf16_t> {
   static constexpr int M = 128, WAVES = YANERF_BF16_WAVES, DXWAVES = YANERF_BF16_DXWAVES, EPC = 8, KB = 32,
-                       APREF = YANERF_BF16_WAVES == 4 ? 2 : 3, LOWREG = YANERF_LOWREG, WPE = LOWREG ? 4 : 2;
+                       APREF = YANERF_BF16_WAVES == 4 ? 2 : 3, LOWREG = YANERF_LOWREG, WPE = LOWREG ? 4 : 2,
+                       HALVES = YANERF_BF16_PP;
   static constexpr int PLANES = 1;
   static constexpr bool PM = YANERF_BF16_PM;
   typedef bf16_t lds_t;
@@ -102,7 +109,7 @@ template <> struct Cfg<bf16_t> {
 #endif
 template <> struct Cfg<x3_t> {
   static constexpr int M = 64, WAVES = 8, DXWAVES = 8, EPC = 8, KB = 32, APREF = YANERF_X3_APREF, LOWREG = 0, WPE = 2,
-                       PLANES = 3;
+                       PLANES = 3, HALVES = 1;
   static constexpr bool PM = false;
   typedef bf16_t lds_t;
   typedef float st_t;
@@ -311,7 +318,14 @@ static int64_t saved_t_bytes(int L, int64_t Npad, size_t es, bool pm) {
 static int64_t tile_m(int prec) {
   return prec == YANERF_PREC_F32 ? Cfg<float>::M : prec == YANERF_PREC_BF16 ? Cfg<bf16_t>::M : Cfg<x3_t>::M;
 }
-static int64_t npad_of(int prec, int64_t n) { int64_t M = tile_m(prec); return (n + M - 1) / M * M; }
+static int64_t fwd_halves(int prec) {
+  return prec == YANERF_PREC_F32 ? Cfg<float>::HALVES : prec == YANERF_PREC_BF16 ? Cfg<bf16_t>::HALVES : Cfg<x3_t>::HALVES;
+}
+// Npad: a multiple of the forward workgroup's points (HALVES tiles of M), so every workgroup holds whole tiles
+static int64_t npad_of(int prec, int64_t n) {
+  const int64_t M = tile_m(prec) * fwd_halves(prec);
+  return (n + M - 1) / M * M;
+}
 // element size of the saved activations / gradient rows (fp32 for both fp32 modes)
 static size_t elem_size(int prec) { return prec == YANERF_PREC_BF16 ? 2 : 4; }
 // element size and plane count of the packed GEMM operands
@@ -1326,7 +1340,8 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // ============================================================================================ forward
 // SAVE: training forward (saved activation rows + ReLU masks for the backward); else inference, outputs only.
 template <typename T, bool SAVE>
-__global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_fwd_kernel(
+__global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
+    __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_fwd_kernel(
     MlpLayout lay, const typename Cfg<T>::w_t* __restrict__ Wt, const float* __restrict__ Wf,
     const float* __restrict__ origins, const float* __restrict__ dirs, const float* __restrict__ lengths, int64_t R,
     int64_t P, float* __restrict__ sigma, float* __restrict__ rgb, typename Cfg<T>::st_t* __restrict__ saved,
@@ -1336,12 +1351,21 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB, TPP = WAVES * 64 / M;  // threads per point
   constexpr int MW = mask_w<T>();  // u64 ReLU-mask words per lane per layer
   typedef typename Cfg<T>::lds_t LT;
-  __shared__ __attribute__((aligned(16))) LT act[Cfg<T>::PLANES * M * ROW];
-  const int tid = threadIdx.x, lane = tid & 63;
+  constexpr int HALVES = Cfg<T>::HALVES;
+  __shared__ __attribute__((aligned(16))) LT act_all[HALVES * Cfg<T>::PLANES * M * ROW];
+  // half h of the workgroup owns point tile `tile` with its own LDS image; everything below is per half
+  const int half = HALVES > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x / (WAVES * 64)) : 0;
+  LT* const act = act_all + half * Cfg<T>::PLANES * M * ROW;
+  const int tid = HALVES > 1 ? (int)threadIdx.x & (WAVES * 64 - 1) : (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int64_t N = R * P;
-  const int64_t p0 = (int64_t)blockIdx.x * M;
+  const int64_t tile = HALVES > 1 ? (int64_t)blockIdx.x * HALVES + half : (int64_t)blockIdx.x;
+  const int64_t ntiles = HALVES > 1 ? (int64_t)gridDim.x * HALVES : (int64_t)gridDim.x;
+  const int64_t p0 = tile * M;
+  // ping-pong: the second half enters one barrier segment late (and the first half leaves with one extra barrier), so
+  // between two workgroup barriers one half runs a layer's GEMM while the other runs its epilogue
+  if (HALVES > 1 && half == 1) lds_barrier();
   typedef typename Cfg<T>::st_t ST;
   const int64_t ld = row_ld(Npad, sizeof(ST)), ldb = ld * (int64_t)sizeof(ST);
   const uint32_t soff = (uint32_t)(4 * g * ldb + li * (int64_t)sizeof(ST));  // this lane's offset in a 16x16 row tile
@@ -1408,7 +1432,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
           save_relu_pm<T, NTHR, 256>(act, 0, (char*)saved + PS.h0 + ((l - 1) * Npad + p0) * 256LL * PM_HB, tid);
 #pragma unroll
           for (int w = 0; w < MW; ++w)
-            masks[((((int64_t)(l - 1) * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
+            masks[((((int64_t)(l - 1) * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
         }
       }
     }
@@ -1437,7 +1461,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     } else if (sv && !(YANERF_ABLATE & 4)) {
 #pragma unroll
       for (int w = 0; w < MW; ++w)
-        masks[((((int64_t)l * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane] = bits[w];
+        masks[((((int64_t)l * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane] = bits[w];
     }
     if (!(YANERF_ABLATE & 32)) lds_barrier();
   }
@@ -1467,7 +1491,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
       save_relu_pm<T, NTHR, 256>(act, 0, (char*)saved + PS.h0 + ((lay.L - 1) * Npad + p0) * 256LL * PM_HB, tid);
 #pragma unroll
       for (int w = 0; w < MW; ++w)
-        masks[((((int64_t)(lay.L - 1) * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
+        masks[((((int64_t)(lay.L - 1) * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
     }
   }
   lds_barrier();
@@ -1512,7 +1536,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
     if constexpr (PM) {
       if (sv) {
         save_grad_pm<T, NTHR, 256, YANERF_BF16_Y8>(act, (char*)saved + PS.y + p0 * 256 * PM_YB,
-                                                   (float*)((char*)saved + PS.ysc) + blockIdx.x, yred, WAVES, tid);
+                                                   (float*)((char*)saved + PS.ysc) + tile, yred, WAVES, tid);
         copy_tile_pm<T, NTHR, KDIR>(act, PE_COL, (ST*)((char*)saved + PS.dpe) + p0 * KDIR, tid);
       }
     }
@@ -1561,6 +1585,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64) __attribute__((amdgpu_wave
   if constexpr (PM) {
     if (sv) save_relu_pm<T, NTHR, HC>(act, 0, (char*)saved + PS.c + p0 * (int64_t)HC * PM_HB, tid);  // C still in LDS
   }
+  if (HALVES > 1 && half == 0) lds_barrier();  // the first half's extra barrier (it entered one segment early)
 }
 
 // ---- the colour layer's direction columns by rays (YANERF_DIRPE_RAY). LinearWithRepeat (nerf_mlp.py) feeds every
@@ -1590,7 +1615,8 @@ template <> __device__ __forceinline__ float lds_val<x3_t>(const bf16_t* act, in
 
 // ============================================================================================ backward dX
 template <typename T>
-__global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_bwd_dx_kernel(
+__global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
+    __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_bwd_dx_kernel(
     MlpLayout lay, const typename Cfg<T>::w_t* __restrict__ Wt, const float* __restrict__ Wf,
     const uint64_t* __restrict__ masks, const float* __restrict__ rgb, const float* __restrict__ g_sigma,
     const float* __restrict__ g_rgb, int64_t N, int64_t Npad, typename Cfg<T>::st_t* __restrict__ grad, int64_t P,
@@ -1606,11 +1632,18 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
   constexpr int KB = Cfg<T>::KB, TPP = WAVES * 64 / M, CPT = HC / TPP;  // colour columns per thread
   static_assert(CPT % 16 == 0, "colour-head backward: whole 16-feature tiles per thread");
   typedef typename Cfg<T>::lds_t LT;
-  __shared__ __attribute__((aligned(16))) LT act[Cfg<T>::PLANES * M * ROW];
-  const int tid = threadIdx.x, lane = tid & 63;
+  // two point tiles per workgroup, the second half one barrier segment behind the first (as the forward, HALVES)
+  constexpr int HALVES = Cfg<T>::HALVES;
+  __shared__ __attribute__((aligned(16))) LT act_all[HALVES * Cfg<T>::PLANES * M * ROW];
+  const int half = HALVES > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x / (WAVES * 64)) : 0;
+  LT* const act = act_all + half * Cfg<T>::PLANES * M * ROW;
+  const int tid = HALVES > 1 ? (int)threadIdx.x & (WAVES * 64 - 1) : (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
-  const int64_t p0 = (int64_t)blockIdx.x * M;
+  const int64_t tile = HALVES > 1 ? (int64_t)blockIdx.x * HALVES + half : (int64_t)blockIdx.x;
+  const int64_t ntiles = HALVES > 1 ? (int64_t)gridDim.x * HALVES : (int64_t)gridDim.x;
+  const int64_t p0 = tile * M;
+  if (HALVES > 1 && half == 1) lds_barrier();
   typedef typename Cfg<T>::st_t ST;
   const int64_t ld = row_ld(Npad, sizeof(ST)), ldb = ld * (int64_t)sizeof(ST);
   const uint32_t soff = (uint32_t)(4 * g * ldb + li * (int64_t)sizeof(ST));  // this lane's offset in a row tile
@@ -1624,7 +1657,7 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
   [[maybe_unused]] char* const gb = (char*)grad;
   [[maybe_unused]] const PmGrad PG = pm_grad(lay.L, Npad);
   [[maybe_unused]] float* const g8red = (float*)(act + 16 * ROW + PE_COL);
-  [[maybe_unused]] float* const g8scl = (float*)(gb + PG.scale) + blockIdx.x;
+  [[maybe_unused]] float* const g8scl = (float*)(gb + PG.scale) + tile;
   [[maybe_unused]] const int64_t ntile = Npad / M;
   auto g8_note = [&](int set, float amax) {  // this wave's |max| of the section being formed
     if constexpr (PM && YANERF_BF16_G8) {
@@ -1792,7 +1825,7 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
     uint64_t bits[MW];
 #pragma unroll
     for (int w = 0; w < MW; ++w)
-      bits[w] = masks[((((int64_t)hl * gridDim.x + blockIdx.x) * WAVES + wave) * MW + w) * 64 + lane];
+      bits[w] = masks[((((int64_t)hl * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane];
     gemm_lds<T, NT, MT, GSX ? 2 : 0>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring,
                              RowSave{(float*)(void*)(grad + (HEAD ? GR.dyx : GR.dz0 + 256LL * l) * ld + p0), soff,
                                      (int)ldb, 256 / KB, wave, WAVES});
@@ -1836,6 +1869,7 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64) __attribute__((amdgpu_wa
   for (int l = lay.L - 1; l >= 1; --l) trunk_step(std::integral_constant<bool, false>{}, l);
   if constexpr (PM && !(YANERF_ABLATE & 128))
     save_grad_pm<T, NTHR, 256>(act, gb + PG.dz0 + p0 * 256 * PM_GB, g8scl, g8red + 8 * ((lay.L + 1) & 1), WAVES, tid);
+  if (HALVES > 1 && half == 0) lds_barrier();
 }
 
 // ============================================================================================ backward dW
@@ -3267,7 +3301,7 @@ static int launch_fwd(const MlpLayout& L, int prec, const void* packed, const fl
   const int64_t Npad = npad_of(prec, N);
   const typename Cfg<T>::w_t* Wt = (const typename Cfg<T>::w_t*)packed;
   const float* Wf = (const float*)((const char*)packed + L.f_base);
-  dim3 grid((unsigned)(Npad / Cfg<T>::M)), block(Cfg<T>::WAVES * 64);
+  dim3 grid((unsigned)(Npad / (Cfg<T>::M * Cfg<T>::HALVES))), block(Cfg<T>::HALVES * Cfg<T>::WAVES * 64);
   uint64_t* masks = saved ? (uint64_t*)((char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM)) : nullptr;
   // bf16 and (with the in-GEMM saves) fp32 inference run the instantiation without the save code
   constexpr bool SPLIT = std::is_same<T, bf16_t>::value || (std::is_same<T, float>::value && YANERF_F32_GSAVE);
@@ -3306,7 +3340,8 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   float* blockp = dzc_part + 2 * (Npad / CH) * HC;
   const uint64_t* masks = (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM));
   if (phase & 1) {
-    hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::DXWAVES * 64), 0, st, L,
+    hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / (Cfg<T>::M * Cfg<T>::HALVES))),
+                       dim3(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64), 0, st, L,
                        Wt, Wf, masks, rgb, gs, gr, N, Npad, gradbuf, P, dir_by_ray ? dzc_part : nullptr);
     YN_LAUNCH_CHECK("mlp_backward_dx");
   }

@@ -266,6 +266,33 @@ def extras(pcfg, cfg, dev, poses, focal, image, precision, others=()):
         "step_mfma_frac": round(train_flops_per_ray(Pc4, Pf4) * R4 / dt / 1e12 / PEAK_TFLOPS["bf16"], 4),
         "fine_fwd_ms": round(f4ms, 4), "fine_fwd_mfma_frac": round(fwd4 / (f4ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"], 4)}
     del tr
+    # the fused step captured as a HIP graph (NeRFTrainer.capture_step / replay_step: bit-equal to the eager step,
+    # tests/test_gpu_trainer.py::test_graph_replayed_steps_equal_eager_steps), eager vs replayed ms per step
+    out["graph_step"] = {}
+    for p in dict.fromkeys(("bf16", precision)):
+        tr = NeRFTrainer(pcfg, precision=p, device=dev, runner_cfg=cfg.runner, train_set_size=LEGO_TRAIN_IMAGES)
+        for i in range(3):
+            tr.step(poses[i:i + 1], focal, image)
+        nst = 20
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(nst):
+            tr.step(poses[(3 + i) % len(poses)][None], focal, image)
+        torch.cuda.synchronize()
+        eager_ms = 1e3 * (time.perf_counter() - t0) / nst
+        tr.capture_step(poses[0:1], focal, image)
+        tr.replay_step(poses[1:2], focal)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(nst):
+            tr.replay_step(poses[(3 + i) % len(poses)][None], focal)
+        torch.cuda.synchronize()
+        graph_ms = 1e3 * (time.perf_counter() - t0) / nst
+        out["graph_step"][p] = {"eager_ms_per_step": round(eager_ms, 4), "graph_ms_per_step": round(graph_ms, 4),
+                                "graph_rays_per_s": round(tr.R / graph_ms * 1e3, 1),
+                                "step_mfma_frac_graph": round(train_flops_per_ray(tr.Pc, tr.Pf) * tr.R / (graph_ms * 1e-3)
+                                                              / 1e12 / PEAK_TFLOPS[p], 4)}
+        del tr
     # BASELINE configs[3] on one GPU: the Fern config (504 x 378, 1024 rays per step) at BASELINE's 64 + 128 samples,
     # LLFF-style per-image depth bounds (a [1, 2] tensor, averaged as ray_sampler.py:280-283 does), synthetic target.
     # Reference CPU path on 8 cores: 341 rays/s

@@ -404,3 +404,41 @@ def test_full_image_800_vs_oracle(precision):
     split_gate(n(f).reshape(-1, 3)[idx], ref["fine"][0], z_gpu, ref["z_fine"], n(d).reshape(-1)[idx],
                ref["fine"][1].reshape(-1), fine_at=fine_at, tag=f"800x800 {precision}",
                coarse=(O, z, n(ro.prev_stage.aux["weights"]), 128))
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_graph_replayed_steps_equal_eager_steps(precision):
+    """hipGraph capture of the fused step (NeRFTrainer.capture_step / replay_step): every per-step scalar (Philox base,
+    Adam's learning rate and bias corrections) is read on the device, so replaying one captured step gives, step after
+    step, bit for bit what eager steps give -- parameters, both Adam moments, losses. The schedule table is shrunk to
+    3 rows so the replays cross two uploads of it; the Lego runner schedule (warm-up) changes the lr every step."""
+    from scene import synthetic_pose
+    from yanerf_amd.train import NeRFTrainer
+    cfg = lego_cfg()
+    trs = [NeRFTrainer(cfg.pipeline, precision=precision, device=DEV, n_rays=512, runner_cfg=cfg.runner, seed=5)
+           for _ in range(2)]
+    for tr in trs:
+        tr.TAB_STEPS = 3
+    img = torch.rand(1, 800, 800, 3, device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
+    poses = [torch.from_numpy(synthetic_pose(20.0 * k, -30.0, 4.0)).float()[None].to(DEV) for k in range(7)]
+    focal = torch.tensor([1111.111], device=DEV)
+    eager, graph = trs
+    losses = []
+    for k in range(7):
+        out = eager.step(poses[k], focal, img)
+        losses.append((out["sq_coarse"].clone(), out["sq_fine"].clone()))
+    graph.step(poses[0], focal, img)  # first launch of every kernel outside the capture
+    graph.capture_step(poses[1], focal, img)
+    for k in range(1, 7):
+        out = graph.replay_step(poses[k], focal)
+        torch.cuda.synchronize()
+        assert torch.equal(out["sq_coarse"], losses[k][0]) and torch.equal(out["sq_fine"], losses[k][1]), k
+    assert graph.step_count == eager.step_count == 7 and graph.lr == eager.lr
+    assert graph.rng.get_state() == eager.rng.get_state()
+    for a, b in ((eager.flat.data, graph.flat.data), (eager.exp_avg, graph.exp_avg), (eager.exp_avg_sq, graph.exp_avg_sq)):
+        assert torch.equal(a, b)
+    # an eager step after the replays continues the same stream
+    a = eager.step(poses[0], focal, img)
+    b = graph.step(poses[0], focal, img)
+    torch.cuda.synchronize()
+    assert torch.equal(a["sq_fine"], b["sq_fine"]) and torch.equal(eager.flat.data, graph.flat.data)

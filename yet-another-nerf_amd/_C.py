@@ -36,7 +36,7 @@ EXPORTS = (
     "yanerf_mlp_pack", "yanerf_mlp_saved_bytes", "yanerf_mlp_bwd_workspace_bytes", "yanerf_mlp_forward",
     "yanerf_mlp_backward", "yanerf_mlp_backward_phase", "yanerf_composite_forward", "yanerf_composite_backward",
     "yanerf_composite_train", "yanerf_sample_pdf",
-    "yanerf_refine", "yanerf_rgb_loss", "yanerf_adam",
+    "yanerf_refine", "yanerf_rgb_loss", "yanerf_adam", "yanerf_adam_scalars", "yanerf_adam_table", "yanerf_step_advance",
 )
 
 
@@ -100,6 +100,9 @@ def lib():
         "yanerf_refine": (c_int, [P, P, i64, i64, i64, c_int, P, c_uint64, c_uint64, c_int, P, P, P]),
         "yanerf_rgb_loss": (c_int, [P, P, P, i64, i64, i64, i64, i64, c_float, P, P, P]),
         "yanerf_adam": (c_int, [P, P, P, P, i64, c_double, c_double, c_double, c_double, c_double, i64, P]),
+        "yanerf_adam_scalars": (c_int, [c_double, c_double, c_double, i64, POINTER(c_float)]),
+        "yanerf_adam_table": (c_int, [P, P, P, P, i64, P, P, c_double, c_double, c_double, c_double, P]),
+        "yanerf_step_advance": (c_int, [P, c_uint64, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

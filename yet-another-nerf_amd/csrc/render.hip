@@ -715,6 +715,33 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   const float denom = sqrtf(vi) / bc2_sqrt + eps;        // _foreach_sqrt; _foreach_div_(bc2_sqrt); _foreach_add_(eps)
   p[i] = __fmaf_rn(neg_step_size, mi / denom, pi);        // _foreach_addcdiv_(params, exp_avgs, denom, -step_size)
 }
+// the same update with the step's two scalars read on the device from a per-step table (row *index): a graph-captured
+// step replays with the schedule's values of the step it runs as
+__global__ void adam_table_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                  float* __restrict__ v, int64_t n, float w1, float b2, float w2, float eps, float wd,
+                                  const float* __restrict__ table, const int64_t* __restrict__ index) {
+  const int64_t k = *index;
+  const float neg_step_size = table[2 * k], bc2_sqrt = table[2 * k + 1];
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float pi = p[i];
+  float gi = g[i];
+  if (wd != 0.0f) gi = __fmaf_rn(wd, pi, gi);
+  const float mi = __fmaf_rn(w1, gi - m[i], m[i]);
+  const float vi = __fmaf_rn(w2, gi * gi, v[i] * b2);
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  p[i] = __fmaf_rn(neg_step_size, mi / denom, pi);
+}
+// end of a step: the Philox base moves past the step's draws and the Adam table index to the next step (one thread;
+// stream-ordered after every kernel of the step that reads them)
+__global__ void step_advance_kernel(uint64_t* state, uint64_t rng_delta) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    state[0] += rng_delta;
+    state[1] += 1;
+  }
+}
 
 }  // namespace yanerf
 
@@ -846,19 +873,47 @@ int yanerf_rgb_loss(const float* pred, const float* image, const float* xys, int
   return 0;
 }
 
-int yanerf_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
-                double beta1, double beta2, double eps, double weight_decay, int64_t step, void* stream) {
+int yanerf_adam_scalars(double lr, double beta1, double beta2, int64_t step, float* out2) {
   YN_CHECK(step >= 1, "adam: step must be >= 1");
-  YN_CHECK(params && grads && exp_avg && exp_avg_sq, "adam: null pointer");
-  if (n == 0) return 0;
+  YN_CHECK(out2, "adam_scalars: null pointer");
   // the host-side scalars in double, as torch computes them in Python (adam.py: bias corrections, step size)
   const double bc1 = 1.0 - std::pow(beta1, (double)step);
   const double bc2 = 1.0 - std::pow(beta2, (double)step);
   const double step_size = lr / bc1;
+  out2[0] = (float)(-step_size);
+  out2[1] = (float)std::sqrt(bc2);
+  return 0;
+}
+
+int yanerf_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
+                double beta1, double beta2, double eps, double weight_decay, int64_t step, void* stream) {
+  YN_CHECK(params && grads && exp_avg && exp_avg_sq, "adam: null pointer");
+  float sc[2];
+  if (yanerf_adam_scalars(lr, beta1, beta2, step, sc)) return 1;
+  if (n == 0) return 0;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), params, grads,
                      exp_avg, exp_avg_sq, n, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
-                     (float)weight_decay, (float)(-step_size), (float)std::sqrt(bc2));
+                     (float)weight_decay, sc[0], sc[1]);
   YN_LAUNCH_CHECK("adam");
+  return 0;
+}
+
+int yanerf_adam_table(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                      const float* table, const int64_t* index, double beta1, double beta2, double eps,
+                      double weight_decay, void* stream) {
+  YN_CHECK(params && grads && exp_avg && exp_avg_sq && table && index, "adam_table: null pointer");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(adam_table_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), params,
+                     grads, exp_avg, exp_avg_sq, n, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
+                     (float)eps, (float)weight_decay, table, index);
+  YN_LAUNCH_CHECK("adam_table");
+  return 0;
+}
+
+int yanerf_step_advance(uint64_t* state, uint64_t rng_delta, void* stream) {
+  YN_CHECK(state, "step_advance: null pointer");
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, as_stream(stream), state, rng_delta);
+  YN_LAUNCH_CHECK("step_advance");
   return 0;
 }
 

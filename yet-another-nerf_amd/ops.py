@@ -275,7 +275,9 @@ class RaymarchCfg:
     hard_background: bool = False
     bg_color: Tuple[float, ...] = (0.0,)
 
-    def opts(self, noise_mode: int = 0, noise_std: float = 0.0, seed: int = 0, offset: int = 0) -> _C.RaymarchOpts:
+    def opts(self, noise_mode: int = 0, noise_std: float = 0.0, seed: int = 0, offset: int = 0,
+             rng_base: Optional[int] = None) -> _C.RaymarchOpts:
+        """rng_base: device address of a u64 added to `offset` by the kernel (the trainer's device step state)."""
         caps = {"exponential": 0, "cap1": 1}
         wfn = {"product": 0, "minimum": 1}
         if self.capping_function not in caps:
@@ -289,7 +291,7 @@ class RaymarchCfg:
         return _C.RaymarchOpts(caps[self.capping_function], wfn[self.weight_function], int(self.blend_output),
                                int(self.hard_background), int(self.density_relu), float(self.background_opacity),
                                float(self.background_density_bias), arr, len(bg), noise_mode, float(noise_std),
-                               seed, offset)
+                               seed, offset, rng_base)
 
 
 class _CompositeFn(torch.autograd.Function):

@@ -160,12 +160,65 @@ class NeRFTrainer:
         self.events: Optional[Dict[str, List]] = None  # optional per-phase timing probes
         self.kernel_probes = False  # serialise the backward kernels (per-kernel timing; see step())
         self.fused_composite = True  # yanerf_composite_train per pass (False: the three separate launches)
+        # device-side step state, so one step is a fixed launch sequence with no per-step host scalars (hipGraph):
+        # [0] the Philox offset base every random kernel adds to its (step-relative) offset, [1] the row of the Adam
+        # table holding this step's (-lr / bias correction 1, sqrt(bias correction 2)); yanerf_step_advance moves
+        # both at the end of each step. The host mirrors them (_dstate_host) and rewrites them only on a mismatch.
+        self._dstate = torch.zeros(2, dtype=torch.int64, device=self.dev)
+        self._dstate_host = None
+        self._tab = torch.empty(self.TAB_STEPS, 2, dtype=F32, device=self.dev)
+        self._tab_base, self._tab_key = 0, None
+        self._pinned_keep: List[torch.Tensor] = []
+        self.graph = None  # capture_step() / replay_step()
+        self._capturing = False
         # evaluation (full-grid rendering) settings of the same configs (ray_sampler.py:54-56; renderer.py:29-52)
         self.Pc_eval = int(rs.get("n_pts_per_ray_evaluation", self.Pc))
         self.Pn_eval = int(rd.get("n_pts_per_ray_fine_evaluation", self.Pn))
         self.stratified_eval = bool(rs.get("stratified_point_sampling_evaluation", False))
         self.random_refine_eval = bool(rd.get("stratified_sampling_coarse_evaluation", False))
         self._eval_ws: Dict[int, Dict[str, torch.Tensor]] = {}
+
+    TAB_STEPS = 1024  # Adam schedule rows uploaded at a time
+
+    # --------------------------------------------------------------------------------------- device step state
+    def _lr_of_step(self, it: int) -> float:
+        if self.runner_cfg is None:
+            return self.lr
+        return lr_at(self.runner_cfg, it, self.world, init_lr=self.init_lr)
+
+    def _pinned(self, t: torch.Tensor) -> torch.Tensor:
+        """A pinned copy of a small host tensor, kept alive until the next sync point (async H2D source)."""
+        p = t.pin_memory() if torch.cuda.is_available() else t
+        self._pinned_keep = self._pinned_keep[-7:] + [p]
+        return p
+
+    def _sync_step_state(self) -> int:
+        """Make the device step state describe the next step (Philox base = the host stream's offset, Adam table row =
+        this step's), uploading the schedule table when the step leaves it or its inputs changed. Returns the host
+        Philox offset at the start of the step. In steady state nothing is uploaded (no host sync)."""
+        seed, off = self.rng.get_state()
+        s = self.step_count
+        key = (None if self.runner_cfg is not None else float(self.lr), float(self.init_lr), tuple(self.betas))
+        if self._tab.shape[0] != self.TAB_STEPS:
+            self._tab, self._tab_key = torch.empty(self.TAB_STEPS, 2, dtype=F32, device=self.dev), None
+        if self._tab_key != key or not (self._tab_base <= s < self._tab_base + self.TAB_STEPS):
+            L = _C.lib()
+            host = torch.empty(self.TAB_STEPS, 2, dtype=F32)
+            base = host.data_ptr()
+            for i in range(self.TAB_STEPS):
+                # the reference schedules before the step (apis.py:66-68); Adam's step count is 1-based
+                _C.check(L.yanerf_adam_scalars(float(self._lr_of_step(s + i)), float(self.betas[0]),
+                                               float(self.betas[1]), s + i + 1,
+                                               ctypes.cast(base + 8 * i, ctypes.POINTER(ctypes.c_float))),
+                         "yanerf_adam_scalars")
+            self._tab.copy_(self._pinned(host), non_blocking=True)
+            self._tab_base, self._tab_key = s, key
+            self._dstate_host = None
+        want = (int(off), s - self._tab_base)
+        if self._dstate_host != want:
+            self._dstate.copy_(self._pinned(torch.tensor(want, dtype=torch.int64)), non_blocking=True)
+            self._dstate_host = want
+        return int(off)
 
     # --------------------------------------------------------------------------------------- timing probes
     def enable_probes(self, names: Sequence[str]):
@@ -240,6 +293,10 @@ class NeRFTrainer:
                                              self.dev)
         L = _C.lib()
         st = ops._stream()
+        if not self._capturing:
+            self._sync_step_state()
+        off0 = self.rng.get_state()[1]  # the device Philox base: kernels get offsets relative to it
+        rbase = ctypes.c_void_p(self._dstate.data_ptr())
         R = self.R
         pose = pose.reshape(1, -1, 4)[:, :3, :4].contiguous()
         focal = focal.reshape(1).contiguous()
@@ -259,8 +316,8 @@ class NeRFTrainer:
         seed, off = self.rng.next(R * self.Pc)
         jmode = 0 if not self.stratified else (1 if inj_jit is not None else 2)
         _C.check(L.yanerf_raygen(_p(pose), _p(focal), None, _p(inj_ids), 1, R, self.W, self.H, float(self.W),
-                                 float(self.H), near, far, self.Pc, jmode, _p(inj_jit), seed, off, _p(self.o),
-                                 _p(self.d), _p(self.zc), _p(self.xys), None, _p(bounds), None, st), "yanerf_raygen")
+                                 float(self.H), near, far, self.Pc, jmode, _p(inj_jit), seed, off - off0, _p(self.o),
+                                 _p(self.d), _p(self.zc), _p(self.xys), None, _p(bounds), rbase, st), "yanerf_raygen")
         scale = 1.0 / (R * C)
         out = {}
         for k, (z, ps) in enumerate(((self.zc, self.passes[0]), (self.zf, self.passes[1]))):
@@ -275,8 +332,8 @@ class NeRFTrainer:
                     if u is not None:
                         u = u.to(self.dev, F32).reshape(R, self.Pn).contiguous()
                     _C.check(L.yanerf_refine(_p(self.zc), _p(self.passes[0].w), R, self.Pc, self.Pn,
-                                             0 if self.random_refine else 1, _p(u), seed, off, int(self.append),
-                                             _p(self.zf), None, st), "yanerf_refine")
+                                             0 if self.random_refine else 1, _p(u), seed, off - off0,
+                                             int(self.append), _p(self.zf), rbase, st), "yanerf_refine")
             P = ps.P
             self._probe(f"mlp_fwd_{k}", lambda: _C.check(L.yanerf_mlp_forward(
                 ctypes.byref(ps.desc), spec.precision, _p(self.packed[k]), _p(self.o), _p(self.d), _p(z), R, P,
@@ -289,7 +346,7 @@ class NeRFTrainer:
                     o = self.march.opts(1, self.noise_std)
                 else:
                     seed, off = self.rng.next(R * P)
-                    o = self.march.opts(2, self.noise_std, seed, off)
+                    o = self.march.opts(2, self.noise_std, seed, off - off0, self._dstate.data_ptr())
             else:
                 o = self.march.opts(0, 0.0)
             if self.fused_composite:
@@ -367,10 +424,71 @@ class NeRFTrainer:
             parallel.allreduce_mean_(self.flat.grad)
         self.lr = self.current_lr()  # the reference schedules before the step (apis.py:66-68)
         self.step_count += 1
-        _C.check(L.yanerf_adam(_p(self.flat.data), _p(self.flat.grad), _p(self.exp_avg), _p(self.exp_avg_sq),
-                               self.flat.numel, float(self.lr), float(self.betas[0]), float(self.betas[1]),
-                               float(self.eps), float(self.weight_decay), self.step_count, st), "yanerf_adam")
+        # Adam with this step's scalars from the device table (the values yanerf_adam computes for this lr and step)
+        _C.check(L.yanerf_adam_table(_p(self.flat.data), _p(self.flat.grad), _p(self.exp_avg), _p(self.exp_avg_sq),
+                                     self.flat.numel, _p(self._tab), ctypes.c_void_p(self._dstate.data_ptr() + 8),
+                                     float(self.betas[0]), float(self.betas[1]), float(self.eps),
+                                     float(self.weight_decay), st), "yanerf_adam_table")
+        delta = self.rng.get_state()[1] - off0
+        _C.check(L.yanerf_step_advance(rbase, delta, st), "yanerf_step_advance")
+        if self._dstate_host is not None:
+            self._dstate_host = (self._dstate_host[0] + delta, self._dstate_host[1] + 1)
         return out
+
+    # --------------------------------------------------------------------------------------- hipGraph
+    def capture_step(self, pose: torch.Tensor, focal: torch.Tensor, image: torch.Tensor, near=None, far=None):
+        """Capture one training step as a HIP graph (torch.cuda.CUDAGraph over the same launch sequence as step()).
+        Every per-step scalar lives on the device (Philox base, Adam table row; _sync_step_state), so replay_step()
+        runs step after step with each step's own draws, learning rate and bias corrections, bit for bit the steps
+        step() would run. pose / focal are copied into static buffers at each replay; the image buffer is captured by
+        reference (replay_step(image=...) copies a different one into it). Run at least one eager step first (the
+        library's kernels load on first launch). Single rank only (a gloo exchange cannot be captured)."""
+        if self.world > 1:
+            raise NotImplementedError("NeRFTrainer.capture_step: single rank only")
+        if self.events is not None or self.kernel_probes:
+            raise ValueError("NeRFTrainer.capture_step: disable timing probes first")
+        self._check_inputs(pose, focal, image)
+        self._g_pose = pose.reshape(1, -1, 4)[:, :3, :4].contiguous().clone()
+        self._g_focal = focal.reshape(1).contiguous().clone()
+        self._g_image = image.reshape(1, self.H, self.W, -1).contiguous()
+        self._g_bounds = (near, far)
+        self._sync_step_state()
+        rng0, step0, lr0, dstate0 = self.rng.get_state(), self.step_count, self.lr, self._dstate_host
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        self._capturing = True
+        try:
+            with torch.cuda.graph(g):
+                out = self.step(self._g_pose, self._g_focal, self._g_image, near, far)
+        finally:
+            self._capturing = False
+        # the capture ran nothing: undo the captured step's host bookkeeping; each replay re-applies it
+        self._g_rng_delta = self.rng.get_state()[1] - rng0[1]
+        self.rng.set_state(rng0)
+        self.step_count, self.lr, self._dstate_host = step0, lr0, dstate0
+        self.graph, self._g_out = g, out
+        return out
+
+    def replay_step(self, pose: Optional[torch.Tensor] = None, focal: Optional[torch.Tensor] = None,
+                    image: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+        """One training step by replaying the captured graph (capture_step), on `pose` / `focal` (copied into the
+        static buffers; default: the previous ones) and the captured image buffer."""
+        if self.graph is None:
+            raise RuntimeError("NeRFTrainer.replay_step: call capture_step first")
+        if pose is not None:
+            self._g_pose.copy_(pose.reshape(1, -1, 4)[:, :3, :4])
+        if focal is not None:
+            self._g_focal.copy_(focal.reshape(1))
+        if image is not None and image.data_ptr() != self._g_image.data_ptr():
+            self._g_image.copy_(image.reshape(self._g_image.shape))
+        self._sync_step_state()  # no-op in steady state; uploads the next schedule rows every TAB_STEPS steps
+        self.lr = self.current_lr()
+        self.graph.replay()
+        seed, off = self.rng.get_state()
+        self.rng.set_state((seed, off + self._g_rng_delta))
+        self.step_count += 1
+        self._dstate_host = (self._dstate_host[0] + self._g_rng_delta, self._dstate_host[1] + 1)
+        return self._g_out
 
     def _mlp_backward(self, k: int, st, stream=None, phase: int = 3):
         L = _C.lib()

@@ -78,6 +78,29 @@ def kernel_flops(kind: str, R: int, P: int) -> float:
     return 2.0 * (MAC_PER_POINT * R * P + MAC_PER_RAY_PASS * R)  # forward and weight gradients
 
 
+def pmc_traffic(kind: str, precision: str):
+    """HBM bytes per fine launch from the committed PMC summary (tools/pmc_summary.py over separate FETCH_SIZE /
+    WRITE_SIZE passes), reported only when that file was collected on the kernel sources this run loaded (its build id
+    equals the library's); a stale file gives traffic null and says so in traffic_source."""
+    from yanerf_amd import _C
+    pmc = ROOT / "profiles" / f"pmc_mlp_{kind}_{precision}.json"
+    src = {"file": str(pmc.relative_to(ROOT)), "build_id": None, "library_build_id": _C.lib().yanerf_build_id().decode()}
+    if not pmc.exists():
+        src["status"] = "missing"
+        return None, src
+    try:
+        d = json.loads(pmc.read_text())
+    except Exception:
+        src["status"] = "unreadable"
+        return None, src
+    src["build_id"] = d.get("build_id")
+    if src["build_id"] != src["library_build_id"]:
+        src["status"] = "stale (collected on other kernel sources)"
+        return None, src
+    src["status"] = "current"
+    return d.get("hbm_bytes_per_launch"), src
+
+
 def kernel_rooflines(tr, poses, focal, image, precision: str, steps: int = 4):
     """Per-kernel HIP-event timings of the fine pass's three MLP kernels (forward, dX walk, dW), each alone on the
     stream: the trainer's probe mode serialises the backward (dX, dW, slab reduce per pass; coarse after fine), so no
@@ -98,16 +121,10 @@ def kernel_rooflines(tr, poses, focal, image, precision: str, steps: int = 4):
         t_ms = ms.get(f"mlp_{kind}_1", float("nan"))
         fl = kernel_flops(kind, R, Pf)
         ach = fl / (t_ms * 1e-3) / 1e12
-        pmc = ROOT / "profiles" / f"pmc_mlp_{kind}_{precision}.json"
-        traffic = None
-        if pmc.exists():
-            try:
-                traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        traffic, source = pmc_traffic(kind, precision)
         out[kind] = {"bound": "mfma", "kernel": f"{kname} (fine pass)", "achieved": round(ach, 2), "peak": peak,
-                     "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic, "flops_per_launch": fl,
-                     "avg_launch_ms": round(t_ms, 4)}
+                     "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic, "traffic_source": source,
+                     "flops_per_launch": fl, "avg_launch_ms": round(t_ms, 4)}
     dom = max(out, key=lambda k: out[k]["avg_launch_ms"])
     serial_ms = {k: round(v, 4) for k, v in ms.items()}
     return out, dom, serial_ms

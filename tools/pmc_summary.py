@@ -11,8 +11,20 @@ read side is doubled (the correction is exact for 16-B-per-lane streams and an u
 import csv
 import glob
 import json
+import importlib.util
 import sys
 from collections import defaultdict
+from pathlib import Path
+
+
+def build_id() -> str:
+    """Build id of the HIP sources these counters were collected on (yanerf_amd/_C.py source_id: the hash the library
+    compiled from them reports), so bench.py can tell whether a PMC file prices the kernels it runs."""
+    root = Path(__file__).resolve().parent.parent
+    spec = importlib.util.spec_from_file_location("_yanerf_C", root / "yet-another-nerf_amd" / "_C.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.source_id()
 
 
 def load(dirname, counter):
@@ -61,7 +73,7 @@ def main():
     fetch_kb = sum(fk) / len(fk)
     write_kb = sum(wk) / len(wk)
     res = {
-        "kernel": kname, "grid_size": gmax_f, "launches": [len(fk), len(wk)],
+        "kernel": kname, "build_id": build_id(), "grid_size": gmax_f, "launches": [len(fk), len(wk)],
         "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
         "hbm_read_bytes_per_launch": 2.0 * fetch_kb * 1024, "hbm_write_bytes_per_launch": write_kb * 1024,
         "hbm_bytes_per_launch": 2.0 * fetch_kb * 1024 + write_kb * 1024,

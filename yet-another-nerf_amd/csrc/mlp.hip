@@ -86,6 +86,12 @@ template <typename T> struct Cfg;
 #ifndef YANERF_BF16_PP
 #define YANERF_BF16_PP 1
 #endif
+// with HALVES = 2: 1 = the second half runs one barrier segment behind the first (GEMM beside epilogue); 0 = both halves
+// in phase (the pair of waves on a SIMD read the same weight fragments at about the same time: one L2 -> CU stream
+// for 256 points)
+#ifndef YANERF_PP_SHIFT
+#define YANERF_PP_SHIFT 1
+#endif
 template <> struct Cfg<float> {
   static constexpr int M = YANERF_F32_M, WAVES = 4, DXWAVES = 4, EPC = 4, KB = 16, APREF = 1, LOWREG = 0,
                        WPE = YANERF_F32_WPE, PLANES = 1, HALVES = 1;
@@ -1365,7 +1371,7 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
   const int64_t p0 = tile * M;
   // ping-pong: the second half enters one barrier segment late (and the first half leaves with one extra barrier), so
   // between two workgroup barriers one half runs a layer's GEMM while the other runs its epilogue
-  if (HALVES > 1 && half == 1) lds_barrier();
+  if (HALVES > 1 && YANERF_PP_SHIFT && half == 1) lds_barrier();
   typedef typename Cfg<T>::st_t ST;
   const int64_t ld = row_ld(Npad, sizeof(ST)), ldb = ld * (int64_t)sizeof(ST);
   const uint32_t soff = (uint32_t)(4 * g * ldb + li * (int64_t)sizeof(ST));  // this lane's offset in a 16x16 row tile
@@ -1585,7 +1591,7 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
   if constexpr (PM) {
     if (sv) save_relu_pm<T, NTHR, HC>(act, 0, (char*)saved + PS.c + p0 * (int64_t)HC * PM_HB, tid);  // C still in LDS
   }
-  if (HALVES > 1 && half == 0) lds_barrier();  // the first half's extra barrier (it entered one segment early)
+  if (HALVES > 1 && YANERF_PP_SHIFT && half == 0) lds_barrier();  // the first half's extra barrier (it entered one segment early)
 }
 
 // ---- the colour layer's direction columns by rays (YANERF_DIRPE_RAY). LinearWithRepeat (nerf_mlp.py) feeds every
@@ -1643,7 +1649,7 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
   const int64_t tile = HALVES > 1 ? (int64_t)blockIdx.x * HALVES + half : (int64_t)blockIdx.x;
   const int64_t ntiles = HALVES > 1 ? (int64_t)gridDim.x * HALVES : (int64_t)gridDim.x;
   const int64_t p0 = tile * M;
-  if (HALVES > 1 && half == 1) lds_barrier();
+  if (HALVES > 1 && YANERF_PP_SHIFT && half == 1) lds_barrier();
   typedef typename Cfg<T>::st_t ST;
   const int64_t ld = row_ld(Npad, sizeof(ST)), ldb = ld * (int64_t)sizeof(ST);
   const uint32_t soff = (uint32_t)(4 * g * ldb + li * (int64_t)sizeof(ST));  // this lane's offset in a row tile
@@ -1869,7 +1875,7 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
   for (int l = lay.L - 1; l >= 1; --l) trunk_step(std::integral_constant<bool, false>{}, l);
   if constexpr (PM && !(YANERF_ABLATE & 128))
     save_grad_pm<T, NTHR, 256>(act, gb + PG.dz0 + p0 * 256 * PM_GB, g8scl, g8red + 8 * ((lay.L + 1) & 1), WAVES, tid);
-  if (HALVES > 1 && half == 0) lds_barrier();
+  if (HALVES > 1 && YANERF_PP_SHIFT && half == 0) lds_barrier();
 }
 
 // ============================================================================================ backward dW
@@ -2908,6 +2914,12 @@ __device__ __forceinline__ void run_pm(const DwJob& J, int k0, int s, int S, int
   // else: not instantiated; launch_bwd refuses a job with such a tile before the launch
 }
 
+// the k-tiles of one point split on one XCD (below): 0 off, 1 fp32 and x3, 2 x3 only. Measured (round 3,
+// profiles/r3_ab_dw_xpair.jsonl): x3 dW 5.69 -> 5.55 ms; fp32 dW 7.62 -> 7.68 ms although its HBM reads drop
+// 24.2 -> 21.5 GB per fine launch (the fp32 dW is not bound by its operand traffic)
+#ifndef YANERF_DW_XPAIR
+#define YANERF_DW_XPAIR 2
+#endif
 template <typename T>
 __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t Npad, int S, float* __restrict__ slab) {
   // x3: two buffers of three 384-row bf16 planes (144 KB); otherwise the LDS-DMA ring
@@ -2922,7 +2934,15 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   while (ji + 1 < jobs.n && jobs.j[ji + 1].tile_base * S <= b) ++ji;
   const DwJob& J = jobs.j[ji];
   const int local = b - J.tile_base * S;
-  const int s = local / J.k_tiles, kt = local % J.k_tiles;
+  int s = local / J.k_tiles, kt = local % J.k_tiles;
+  if ((YANERF_DW_XPAIR == 1 || (YANERF_DW_XPAIR == 2 && is_x3<T>)) && !Cfg<T>::PM && (S & 7) == 0 && J.k_tiles > 1) {
+    // the k-tiles of one split 8 blocks apart: blocks go to the 8 XCDs round robin, so every k-tile that stages the
+    // split's dZ rows runs on the same XCD (one L2) at about the same time (block b's XCD is b % 8 and tile_base * S
+    // is a multiple of 8)
+    const int grp = local / (8 * J.k_tiles), r = local % (8 * J.k_tiles);
+    kt = r >> 3;
+    s = grp * 8 + (r & 7);
+  }
   constexpr int BKMAX = dw_bkmax(prec_of<T>);
   const int k0 = kt * BKMAX;
   const int bk = kt < J.k_full ? BKMAX : J.bk_tail;

@@ -25,7 +25,30 @@ __device__ __forceinline__ void valu(v2f (&v)[16], v2f x, v2f y) {
   for (int i = 0; i < NV; ++i) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(v[i % 16]) : "v"(x), "v"(y));
 }
 
-template <int MODE, int NV>
+// OP (MODE 3 only): 0 v_pk_fma_f32, 1 v_add_u32, 2 v_mov_b32, 3 v_fma_f32, 4 v_xor_b32 -- which VALU ops take issue
+// slots from the f32 MFMA
+template <int OP, int NV>
+__device__ __forceinline__ void valu_op(v2f (&v)[16], v2f x, v2f y) {
+  if constexpr (OP == 0) {
+    valu<NV>(v, x, y);
+  } else {
+    float f[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) f[i] = v[i].x;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      float& d = f[i % 16];
+      if constexpr (OP == 1) asm volatile("v_add_u32 %0, %0, %1" : "+v"(d) : "v"(y.x));
+      if constexpr (OP == 2) asm volatile("v_mov_b32 %0, %1" : "=v"(d) : "v"(f[(i + 1) % 16]));
+      if constexpr (OP == 3) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(d) : "v"(x.x), "v"(y.x));
+      if constexpr (OP == 4) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(d) : "v"(y.x));
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i].x = f[i];
+  }
+}
+
+template <int MODE, int NV, int OP = 0>
 __global__ void __launch_bounds__(512) k(float* out, float s) {
   const int wave = threadIdx.x >> 6;
   v4f c[8];
@@ -39,7 +62,7 @@ __global__ void __launch_bounds__(512) k(float* out, float s) {
   if (do_mfma && do_valu) {
     for (int it = 0; it < ITERS; ++it) {
       mfma8(c, a, b);
-      valu<NV>(v, x, y);
+      valu_op<OP, NV>(v, x, y);
     }
   } else if (do_mfma) {
     for (int it = 0; it < ITERS; ++it) mfma8(c, a, b);
@@ -52,15 +75,15 @@ __global__ void __launch_bounds__(512) k(float* out, float s) {
   out[blockIdx.x * 512 + threadIdx.x] = r;
 }
 
-template <int MODE, int NV>
+template <int MODE, int NV, int OP = 0>
 static void run(const char* name, float* out, int grid) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  k<MODE, NV><<<grid, 512>>>(out, 1.0f);
+  k<MODE, NV, OP><<<grid, 512>>>(out, 1.0f);
   hipEventRecord(e0);
   const int reps = 5;
-  for (int r = 0; r < reps; ++r) k<MODE, NV><<<grid, 512>>>(out, 1.0f);
+  for (int r = 0; r < reps; ++r) k<MODE, NV, OP><<<grid, 512>>>(out, 1.0f);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms;
@@ -74,8 +97,8 @@ static void run(const char* name, float* out, int grid) {
   if (MODE == 2) mf_waves = va_waves = waves / 2;
   if (MODE == 3) mf_waves = va_waves = waves;
   const double fl_m = mf_waves * 8.0 * ITERS * 2048.0, fl_v = va_waves * (double)NV * ITERS * 256.0;
-  printf("{\"case\": \"%s\", \"nv\": %d, \"ms\": %.4f, \"mfma_tflops\": %.2f, \"valu_tflops\": %.2f, \"total_tflops\": %.2f}\n",
-         name, NV, ms, fl_m / ms / 1e9, fl_v / ms / 1e9, (fl_m + fl_v) / ms / 1e9);
+  printf("{\"case\": \"%s\", \"op\": %d, \"nv\": %d, \"ms\": %.4f, \"mfma_tflops\": %.2f, \"valu_tflops\": %.2f, \"total_tflops\": %.2f}\n",
+         name, OP, NV, ms, fl_m / ms / 1e9, fl_v / ms / 1e9, (fl_m + fl_v) / ms / 1e9);
 }
 
 int main() {
@@ -92,6 +115,15 @@ int main() {
   run<3, 8>("mixed", out, grid);
   run<3, 16>("mixed", out, grid);
   run<3, 32>("mixed", out, grid);
+  // MFMA throughput with 8 and 16 VALU ops of each kind per 8 MFMAs (valu_tflops only meaningful for op 0 / 3)
+  run<3, 8, 1>("mixed", out, grid);
+  run<3, 16, 1>("mixed", out, grid);
+  run<3, 8, 2>("mixed", out, grid);
+  run<3, 16, 2>("mixed", out, grid);
+  run<3, 8, 3>("mixed", out, grid);
+  run<3, 16, 3>("mixed", out, grid);
+  run<3, 8, 4>("mixed", out, grid);
+  run<3, 16, 4>("mixed", out, grid);
   hipFree(out);
   return 0;
 }

@@ -2771,6 +2771,12 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
 // current one multiplies), split into three bf16 planes on the way into LDS (same 64-byte rows and swizzle as the
 // bf16 dW tile) and multiplied with the six plane products per 16x16x32 step. Two LDS buffers, one barrier per
 // stage. Bias gradients are fp32 row sums of the loaded dZ segments.
+// x3 dW: software-pipelined staging (1) or split-then-multiply per stage (0). Measured equal (round 3,
+// profiles/r3_ab_x3_dw_pipe.jsonl: 5.41 / 5.42 vs 5.41 / 5.40 ms, bitwise-equal gradients): the split is not what
+// the x3 dW waits on
+#ifndef YANERF_X3_DWPIPE
+#define YANERF_X3_DWPIPE 0
+#endif
 template <int BN, int BK>
 __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S, int64_t Npad,
                                            float* __restrict__ slab, int64_t slab_elems, char* smem) {
@@ -2818,28 +2824,88 @@ __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S,
   for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
     for (int q = 0; q < KTW; ++q) acc[nt][q] = zero;
-  if (st_lo < st_hi) load(st_lo);
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  // split staged segment i (fp32) into the three bf16 planes of buffer `buf` (+ the bias row sums)
+  auto split_one = [&](int i, char* buf) {
+    if (dst[i] >= 0) {
+      const f4 v0 = regs[i];
+      if (do_bias && (tid + DW_THREADS * i) / 8 < BN) rsum[i] += (v0.x + v0.y) + (v0.z + v0.w);
+      const Pk<bf16_t> h0 = pk_make<bf16_t>(v0);
+      const f4 r1 = v0 - f4{__uint_as_float(h0.w0 << 16), __uint_as_float(h0.w0 & 0xffff0000u),
+                            __uint_as_float(h0.w1 << 16), __uint_as_float(h0.w1 & 0xffff0000u)};
+      const Pk<bf16_t> h1 = pk_make<bf16_t>(r1);
+      const f4 r2 = r1 - f4{__uint_as_float(h1.w0 << 16), __uint_as_float(h1.w0 & 0xffff0000u),
+                            __uint_as_float(h1.w1 << 16), __uint_as_float(h1.w1 & 0xffff0000u)};
+      const Pk<bf16_t> h2 = pk_make<bf16_t>(r2);
+      *(u32x2*)(buf + dst[i]) = u32x2{h0.w0, h0.w1};
+      *(u32x2*)(buf + PLB + dst[i]) = u32x2{h1.w0, h1.w1};
+      *(u32x2*)(buf + 2 * PLB + dst[i]) = u32x2{h2.w0, h2.w1};
+    }
+  };
+  if constexpr (YANERF_X3_DWPIPE) {
+    // software-pipelined stages: while a wave multiplies stage st from one buffer it splits stage st + 1 (loaded during
+    // stage st - 1) into the other, one staged segment after each of the six product terms, and reloads that segment's
+    // registers with stage st + 2 right away; one barrier per stage. (Unpipelined, every wave split its segments
+    // between two barriers with no MFMA in flight on its SIMD.) Each accumulator still sees the stages in order and the
+    // same six terms per stage: gradients bitwise equal.
+    static_assert(LPT <= 6, "x3 dW pipeline: one staged segment per product term");
+    if (st_lo < st_hi) {
+      load(st_lo);
+#pragma unroll
+      for (int i = 0; i < LPT; ++i) split_one(i, smem + (int)(st_lo & 1) * BUFB);
+      if (st_lo + 1 < st_hi) load(st_lo + 1);
+    }
+    __syncthreads();
+    for (int64_t st = st_lo; st < st_hi; ++st) {
+      char* buf = smem + (int)(st & 1) * BUFB;
+      char* nbuf = smem + (int)((st + 1) & 1) * BUFB;
+      const bool nxt = st + 1 < st_hi, nxt2 = st + 2 < st_hi;
+      if (mma_wave) {
+        f4 a[3][4];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            const int row = wn * 64 + 16 * nt + li;
+            a[pl][nt] = *(const f4*)(buf + pl * PLB + row * 64 + (dw_swz4(row, g) << 4));
+          }
+        static_assert(KTW <= 4, "x3 dW pipeline: one column-fragment group");
+        f4 b[3][KTW];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+          for (int q = 0; q < KTW; ++q) {
+            const int row = BN + (wk * KTW + q) * 16 + li;
+            b[pl][q] = *(const f4*)(buf + pl * PLB + row * 64 + (dw_swz4(row, g) << 4));
+          }
+        constexpr int TI[6] = {2, 1, 0, 1, 0, 0}, TJ[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+            for (int q = 0; q < KTW; ++q) acc[nt][q] = mma_blk<bf16_t>(a[TI[t]][nt], b[TJ[t]][q], acc[nt][q]);
+          if (t < LPT) {
+            if (nxt) split_one(t, nbuf);
+            if (nxt2) regs[t] = *(const f4*)(src[t] + (st + 2) * X3_SPTS);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < LPT; ++i) {
+          if (nxt) split_one(i, nbuf);
+          if (nxt2) regs[i] = *(const f4*)(src[i] + (st + 2) * X3_SPTS);
+        }
+      }
+      __syncthreads();
+    }
+  } else {
+  if (st_lo < st_hi) load(st_lo);
   for (int64_t st = st_lo; st < st_hi; ++st) {
     char* buf = smem + (int)(st & 1) * BUFB;
     // split the staged fp32 segments into the three planes of this stage's buffer
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      if (dst[i] >= 0) {
-        const f4 v0 = regs[i];
-        if (do_bias && (tid + DW_THREADS * i) / 8 < BN) rsum[i] += (v0.x + v0.y) + (v0.z + v0.w);
-        const Pk<bf16_t> h0 = pk_make<bf16_t>(v0);
-        const f4 r1 = v0 - f4{__uint_as_float(h0.w0 << 16), __uint_as_float(h0.w0 & 0xffff0000u),
-                              __uint_as_float(h0.w1 << 16), __uint_as_float(h0.w1 & 0xffff0000u)};
-        const Pk<bf16_t> h1 = pk_make<bf16_t>(r1);
-        const f4 r2 = r1 - f4{__uint_as_float(h1.w0 << 16), __uint_as_float(h1.w0 & 0xffff0000u),
-                              __uint_as_float(h1.w1 << 16), __uint_as_float(h1.w1 & 0xffff0000u)};
-        const Pk<bf16_t> h2 = pk_make<bf16_t>(r2);
-        *(u32x2*)(buf + dst[i]) = u32x2{h0.w0, h0.w1};
-        *(u32x2*)(buf + PLB + dst[i]) = u32x2{h1.w0, h1.w1};
-        *(u32x2*)(buf + 2 * PLB + dst[i]) = u32x2{h2.w0, h2.w1};
-      }
-    }
+    for (int i = 0; i < LPT; ++i) split_one(i, buf);
     __syncthreads();
     if (st + 1 < st_hi) load(st + 1);
     if (mma_wave) {
@@ -2872,6 +2938,7 @@ __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S,
               acc[nt][q0 + q] = mma_blk<bf16_t>(a[TI[t]][nt], b[TJ[t]][q], acc[nt][q0 + q]);
       }
     }
+  }
   }
   float* out = slab + (int64_t)s * slab_elems + J.slab_off;
   const int kv = J.ktot + 1;

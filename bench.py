@@ -217,6 +217,15 @@ def extras(pcfg, cfg, dev, poses, focal, image, precision, others=()):
     dt = time.perf_counter() - t0
     out["eval_render_fused"] = {"rays_per_s": round(H * W / dt, 1), "s_per_image": round(dt, 3),
                                 "chunk_rays": 65536, "precision": precision}
+    # the same render as one HIP-graph launch per image (NeRFTrainer.render_graph, bitwise equal)
+    tr.render_graph(poses[:1], focal, H, W)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tr.render_graph(poses[1:2], focal, H, W)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out["eval_render_graph"] = {"rays_per_s": round(H * W / dt, 1), "s_per_image": round(dt, 3),
+                                "launches_per_image": 1, "precision": precision}
     del tr
     # the fused evaluation render in every precision mode, with its whole-image MFMA utilisation (inference FLOPs:
     # 2 x (589,952 MAC/point x (Pc + Pc + Pf) points + 3,456 MAC/ray/pass x 2) per ray)

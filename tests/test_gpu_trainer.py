@@ -442,3 +442,23 @@ def test_graph_replayed_steps_equal_eager_steps(precision):
     b = graph.step(poses[0], focal, img)
     torch.cuda.synchronize()
     assert torch.equal(a["sq_fine"], b["sq_fine"]) and torch.equal(eager.flat.data, graph.flat.data)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_graph_render_equals_eager_render(precision):
+    """NeRFTrainer.render_graph: the whole chunked evaluation render of an image captured as one HIP graph and
+    replayed per camera (one graph launch per image) gives bit for bit render()'s images, for the captured camera and
+    for a different one copied into the graph's static inputs, over a ragged last chunk."""
+    from scene import synthetic_pose
+    from yanerf_amd.train import NeRFTrainer
+    cfg = lego_cfg()
+    tr = NeRFTrainer(cfg.pipeline, precision=precision, device=DEV, n_rays=256, seed=3)
+    focal = torch.tensor([1111.111 * 120 / 800], device=DEV)
+    poses = [torch.from_numpy(synthetic_pose(35.0 * k, -30.0, 4.0)).float()[None].to(DEV) for k in range(3)]
+    H = W = 120  # 14,400 rays: chunks of 4096, the last one ragged
+    for k in (0, 1, 2, 1):
+        ef, ec, ed = (t.clone() for t in tr.render(poses[k], focal, H, W, chunk=4096))
+        gf, gc, gd = tr.render_graph(poses[k], focal, H, W, chunk=4096)
+        torch.cuda.synchronize()
+        assert torch.equal(ef, gf) and torch.equal(ec, gc) and torch.equal(ed, gd), k
+    assert tr._render_graph is not None and tr._render_graph[0] == (H, W, None, None, 4096)

@@ -170,6 +170,7 @@ class NeRFTrainer:
         self._tab_base, self._tab_key = 0, None
         self._pinned_keep: List[torch.Tensor] = []
         self.graph = None  # capture_step() / replay_step()
+        self._render_graph = None  # render_graph(): (key, graph, static pose, static focal, static outputs)
         self._capturing = False
         # evaluation (full-grid rendering) settings of the same configs (ray_sampler.py:54-56; renderer.py:29-52)
         self.Pc_eval = int(rs.get("n_pts_per_ray_evaluation", self.Pc))
@@ -577,6 +578,36 @@ class NeRFTrainer:
         if world > 1:
             out_f, out_c, out_d = (parallel.gather_rows(t, H) for t in (out_f, out_c, out_d))
         return out_f, out_c, out_d
+
+    @torch.no_grad()
+    def render_graph(self, pose: torch.Tensor, focal: torch.Tensor, H: Optional[int] = None, W: Optional[int] = None,
+                     near: Optional[float] = None, far: Optional[float] = None, chunk: int = 65536):
+        """render() as ONE graph launch per image: the first call for an (H, W, near, far, chunk) captures the whole
+        chunk loop (weight pack, per chunk raygen -> coarse MLP -> composite -> refine -> fine MLP -> composite, and
+        the output copies; nerf_pipeline.py:217-236, 327-377) into a HIP graph, later calls copy pose / focal into its
+        static inputs and replay it. Bit for bit render() (tests/test_gpu_trainer.py). The reference's evaluation
+        sampling is deterministic (no stratified depths, deterministic refinement); a config with random evaluation
+        draws would freeze them in the graph, so it is refused. Single rank; the returned tensors are the graph's
+        static outputs, overwritten by the next replay."""
+        if self.stratified_eval or self.random_refine_eval:
+            raise NotImplementedError("NeRFTrainer.render_graph: random evaluation sampling cannot be replayed")
+        key = (int(H or self.H), int(W or self.W), near, far, int(chunk))
+        if self._render_graph is None or self._render_graph[0] != key:
+            sp = pose.reshape(1, -1, 4)[:, :3, :4].contiguous().clone()
+            sf = focal.reshape(1).contiguous().clone()
+            self.render(sp, sf, *key[:4], chunk=chunk)  # eager first: the evaluation buffers exist before the capture
+            torch.cuda.synchronize(self.dev)
+            rng0 = self.rng.get_state()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                outs = self.render(sp, sf, *key[:4], chunk=chunk)
+            self.rng.set_state(rng0)  # deterministic draws: the counter only keeps render()'s bookkeeping
+            self._render_graph = (key, g, sp, sf, outs)
+        _, g, sp, sf, outs = self._render_graph
+        sp.copy_(pose.reshape(1, -1, 4)[:, :3, :4])
+        sf.copy_(focal.reshape(1))
+        g.replay()
+        return outs
 
     def evaluate(self, images, shard: bool = True) -> Dict[str, float]:
         """Render every camera of a DeviceImageSet and score it as the reference's eval_one_epoch + create_stats do:

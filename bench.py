@@ -101,10 +101,13 @@ def pmc_traffic(kind: str, precision: str):
     return d.get("hbm_bytes_per_launch"), src
 
 
-def kernel_rooflines(tr, poses, focal, image, precision: str, steps: int = 4):
+def kernel_rooflines(tr, poses, focal, image, precision: str, steps: int = 4, live=None):
     """Per-kernel HIP-event timings of the fine pass's three MLP kernels (forward, dX walk, dW), each alone on the
-    stream: the trainer's probe mode serialises the backward (dX, dW, slab reduce per pass; coarse after fine), so no
-    kernel shares the GPU while it is timed. Returns {kernel: roofline dict} and the dominant kernel by time."""
+    stream. `live` = the event timings taken inside the timed steps (the forwards always; in the serial-backward modes,
+    fp32 and fp32x3, the dX and dW launches too): a kernel timed there is priced on that average ("timing": "timed
+    steps"). The others come from a few steps in the trainer's probe mode after the timed region, which serialises the
+    backward (dX, dW, slab reduce per pass; coarse after fine), so no kernel shares the GPU while it is timed
+    ("timing": "probe steps"). Returns {kernel: roofline dict}, the dominant kernel by time, the probe-step timings."""
     tr.kernel_probes = True
     names = ["mlp_fwd_1", "mlp_dx_1", "mlp_dw_1", "mlp_reduce_1", "mlp_fwd_0", "mlp_dx_0", "mlp_dw_0", "mlp_reduce_0"]
     tr.enable_probes(names)
@@ -117,14 +120,16 @@ def kernel_rooflines(tr, poses, focal, image, precision: str, steps: int = 4):
     R, Pf = tr.R, tr.Pf
     peak = PEAK_TFLOPS[precision]
     out = {}
+    live = live or {}
     for kind, kname in (("fwd", "mlp_fwd_kernel"), ("dx", "mlp_bwd_dx_kernel"), ("dw", "mlp_dw_kernel")):
-        t_ms = ms.get(f"mlp_{kind}_1", float("nan"))
+        how = "timed steps" if f"mlp_{kind}_1" in live else "probe steps"
+        t_ms = live.get(f"mlp_{kind}_1", ms.get(f"mlp_{kind}_1", float("nan")))
         fl = kernel_flops(kind, R, Pf)
         ach = fl / (t_ms * 1e-3) / 1e12
         traffic, source = pmc_traffic(kind, precision)
         out[kind] = {"bound": "mfma", "kernel": f"{kname} (fine pass)", "achieved": round(ach, 2), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic, "traffic_source": source,
-                     "flops_per_launch": fl, "avg_launch_ms": round(t_ms, 4)}
+                     "flops_per_launch": fl, "avg_launch_ms": round(t_ms, 4), "timing": how}
     dom = max(out, key=lambda k: out[k]["avg_launch_ms"])
     serial_ms = {k: round(v, 4) for k, v in ms.items()}
     return out, dom, serial_ms
@@ -457,7 +462,10 @@ def main():
             tr.step(poses[(i + rank) % len(poses)][None], focal, image)
         if probes:  # HIP events around the two forward launches (they have the GPU to themselves) and, at N > 1,
             # around the wait for the gradient exchange on the compute stream (its exposed part)
-            tr.enable_probes(["mlp_fwd_0", "mlp_fwd_1"] + (["allreduce_exposed"] if world > 1 else []))
+            names = ["mlp_fwd_0", "mlp_fwd_1"] + (["allreduce_exposed"] if world > 1 else [])
+            if tr.side is None and world == 1:  # serial backward: its dX / dW launches are timed in place as well
+                names += [f"mlp_{k}_{i}" for i in (1, 0) for k in ("dx", "dw", "reduce")]
+            tr.enable_probes(names)
         parallel.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -483,7 +491,7 @@ def main():
     flops_ray = train_flops_per_ray(Pc, Pf)
     # per-kernel rooflines of the fine pass (each kernel timed alone, after the timed region); `roofline` is the
     # dominant kernel by time, the others are listed beside it
-    rk, dom, serial_ms = kernel_rooflines(tr, poses, focal, image, args.precision)
+    rk, dom, serial_ms = kernel_rooflines(tr, poses, focal, image, args.precision, live=probe)
     peak = PEAK_TFLOPS[args.precision]
     result = {
         "metric": METRIC,
@@ -504,7 +512,7 @@ def main():
         "roofline_kernels": rk,
         "step_mfma_tflops": round(flops_ray * value / world / 1e12, 2),
         "step_mfma_frac": round(flops_ray * value / world / 1e12 / peak, 4),
-        "fwd_ms_in_timed_steps": {k: round(v, 4) for k, v in probe.items() if k.startswith("mlp_")},
+        "kernel_ms_in_timed_steps": {k: round(v, 4) for k, v in probe.items() if k.startswith("mlp_")},
         "kernel_ms_serialised": serial_ms,
     }
     if dist_info is not None:
@@ -522,14 +530,14 @@ def main():
         tr2, dt2, _ = run(p2name, args.steps, args.warmup, probes=True)
         v2 = R * world * args.steps / dt2
         fwd2 = {k: round(v, 4) for k, v in tr2.probe_ms().items()}
-        rk2, dom2, serial2 = kernel_rooflines(tr2, poses, focal, image, p2name)
+        rk2, dom2, serial2 = kernel_rooflines(tr2, poses, focal, image, p2name, live=tr2.probe_ms())
         result["secondary"][p2name] = {
             "value": round(v2, 1), "unit": "rays/s",
             "ms_per_step": round(1e3 * dt2 / args.steps, 3),
             "roofline": rk2[dom2],
             "roofline_kernels": rk2,
             "step_mfma_frac": round(flops_ray * v2 / world / 1e12 / PEAK_TFLOPS[p2name], 4),
-            "fwd_ms_in_timed_steps": fwd2,
+            "kernel_ms_in_timed_steps": fwd2,
             "kernel_ms_serialised": serial2,
             "note": notes[p2name],
         }

@@ -400,8 +400,15 @@ class NeRFTrainer:
                 for ph in (1, 4, 8):
                     self._mlp_backward(k, st, phase=ph)
         elif self.side is None:
-            self._mlp_backward(1, st)
-            self._mlp_backward(0, st)
+            if self.events is not None and any(n.startswith(("mlp_dx_", "mlp_dw_")) for n in self.events):
+                # serial backward with timing probes (bench.py's live per-kernel roofline): the same kernels in the
+                # same order as one phase-3 call, issued phase by phase so each gets its own event pair
+                for k in (1, 0):
+                    for ph in (1, 4, 8):
+                        self._mlp_backward(k, st, phase=ph)
+            else:
+                self._mlp_backward(1, st)
+                self._mlp_backward(0, st)
         elif self.overlap == "early":
             self._mlp_backward(1, st)
             torch.cuda.current_stream().wait_stream(self.side)

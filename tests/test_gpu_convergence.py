@@ -114,3 +114,59 @@ def test_fused_trainer_converges(precision):
     print(f"{precision}: fused-trainer loss {first:.4f} -> {last:.4f}")
     assert np.isfinite(losses).all()
     assert last < 0.02 * first, (first, last)  # measured ~1e-3 of the first loss in every mode
+
+
+def test_trained_activations_stay_below_fp8_clamp(tmp_path):
+    """The bf16 mode stores the post-ReLU activations H_0..H_7 and C for the weight gradients as fp8 e4m3 WITHOUT a
+    scale, clamped at 448 (a value above it would give a wrong weight gradient). This pins the assumption
+    on trained weights: the fused bf16 trainer fits the procedural nerf_synthetic-format scene (tools/synthetic_scene,
+    Lego config, 1,500 steps), then the oracle evaluates its fp32 master weights on the rays of a test view and every
+    trunk / colour-hidden activation must stay below 448 / 8 (a margin of 8x). The maxima go to the parity report."""
+    import sys
+    from pathlib import Path
+
+    import yanerf_boot  # noqa: F401
+    from oracle import nerf_oracle as O
+    from parity_gates import write_report
+    from weights import LEGO_ARCH
+    root = Path(__file__).resolve().parents[1]
+    sys.path.insert(0, str(root / "tools"))
+    from synthetic_scene import write_scene
+    from yanerf_amd.datasets import BlenderDataset, DeviceImageSet
+    from yanerf_amd.train import NeRFTrainer
+    from yanerf_amd.utils.config import Config
+
+    data = write_scene(tmp_path / "scene", 64, 20, 2, device=DEV)
+    train = DeviceImageSet(BlenderDataset(str(data), "train"), DEV)
+    cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml"))
+    pcfg = cfg.pipeline
+    pcfg.ray_sampler.image_height, pcfg.ray_sampler.image_width = train.H, train.W
+    runner = dict(cfg.runner)
+    steps = 1500
+    runner["warmup_steps"], runner["lr_decay_iters"] = steps // 10, steps * 1.25
+    tr = NeRFTrainer(pcfg, precision="bf16", device=DEV, runner_cfg=runner, seed=7)
+    it, epoch = 0, 0
+    while it < steps:
+        for i in train.epoch_order(epoch, seed=7):
+            if it >= steps:
+                break
+            pose, focal, img, _, _ = train.item(i)
+            tr.step(pose, focal, img)
+            it += 1
+        epoch += 1
+    torch.cuda.synchronize()
+    arch = O.MLPArch.from_dict(LEGO_ARCH)
+    pose, focal, _, _, _ = train.item(0)
+    pose_np = pose.reshape(1, 3, 4).cpu().numpy()
+    o, d, z, _ = O.sample_rays_eval(pose_np, focal.reshape(1).cpu().numpy(), train.W, train.H, tr.near, tr.far, 64)
+    o, d, z = o.reshape(-1, 3), d.reshape(-1, 3), z.reshape(-1, 64)
+    rows = np.arange(0, o.shape[0], 16)  # 256 rays of the view
+    maxima = {}
+    for k, model in enumerate(tr.models):
+        params = {n: p.detach().cpu().numpy() for n, p in model.state_dict().items()}
+        _, _, cache = O.nerf_mlp_forward(params, arch, o[rows], d[rows], z[rows])
+        maxima[("coarse", "fine")[k]] = [float(h.max()) for h in cache.layer_out] + [float(cache.c0.max())]
+    write_report("activation_range", "bf16 trained 1500 steps, procedural scene", {"max_post_relu": maxima,
+                                                                                   "fp8_clamp": 448.0})
+    worst = max(max(v) for v in maxima.values())
+    assert np.isfinite(worst) and worst < 448.0 / 8, maxima

@@ -542,7 +542,9 @@ def main():
             "note": notes[p2name],
         }
         del tr2
-    if not args.no_extras:
+    if not args.no_extras and world == 1:
+        # single-GPU characteristics (evaluation render, drop-in path, other configs, graph replay): at N > 1 every rank
+        # would repeat them, and the graph capture is single-rank by design
         result["extras"] = extras(pcfg, cfg, dev, poses, focal, image, args.precision, tuple(sec))
     if rank == 0 and world == 1 and args.psnr_steps > 0:
         result["psnr"] = psnr_leg(args.precision, args.psnr_steps, dev)

@@ -461,4 +461,6 @@ def test_graph_render_equals_eager_render(precision):
         gf, gc, gd = tr.render_graph(poses[k], focal, H, W, chunk=4096)
         torch.cuda.synchronize()
         assert torch.equal(ef, gf) and torch.equal(ec, gc) and torch.equal(ed, gd), k
+        if k == 2:  # an eager render of another chunk size replaces the eager buffer cache; the graph keeps its own
+            tr.render(poses[0], focal, 40, 40, chunk=512)
     assert tr._render_graph is not None and tr._render_graph[0] == (H, W, None, None, 4096)

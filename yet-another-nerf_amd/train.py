@@ -170,7 +170,7 @@ class NeRFTrainer:
         self._tab_base, self._tab_key = 0, None
         self._pinned_keep: List[torch.Tensor] = []
         self.graph = None  # capture_step() / replay_step()
-        self._render_graph = None  # render_graph(): (key, graph, static pose, static focal, static outputs)
+        self._render_graph = None  # render_graph(): (key, graph, static pose/focal, static outputs, buffers)
         self._capturing = False
         # evaluation (full-grid rendering) settings of the same configs (ray_sampler.py:54-56; renderer.py:29-52)
         self.Pc_eval = int(rs.get("n_pts_per_ray_evaluation", self.Pc))
@@ -598,7 +598,8 @@ class NeRFTrainer:
         static outputs, overwritten by the next replay."""
         if self.stratified_eval or self.random_refine_eval:
             raise NotImplementedError("NeRFTrainer.render_graph: random evaluation sampling cannot be replayed")
-        key = (int(H or self.H), int(W or self.W), near, far, int(chunk))
+        key = (int(H or self.H), int(W or self.W), None if near is None else float(near),
+               None if far is None else float(far), int(chunk))
         if self._render_graph is None or self._render_graph[0] != key:
             sp = pose.reshape(1, -1, 4)[:, :3, :4].contiguous().clone()
             sf = focal.reshape(1).contiguous().clone()
@@ -609,8 +610,11 @@ class NeRFTrainer:
             with torch.cuda.graph(g):
                 outs = self.render(sp, sf, *key[:4], chunk=chunk)
             self.rng.set_state(rng0)  # deterministic draws: the counter only keeps render()'s bookkeeping
-            self._render_graph = (key, g, sp, sf, outs)
-        _, g, sp, sf, outs = self._render_graph
+            # the graph writes into these evaluation buffers: keep them alive even if a later eager render() of
+            # another size replaces the trainer's buffer cache
+            keep = dict(self._eval_ws)
+            self._render_graph = (key, g, sp, sf, outs, keep)
+        _, g, sp, sf, outs, _ = self._render_graph
         sp.copy_(pose.reshape(1, -1, 4)[:, :3, :4])
         sf.copy_(focal.reshape(1))
         g.replay()

@@ -353,6 +353,51 @@ def extras(pcfg, cfg, dev, poses, focal, image, precision, others=()):
     return out
 
 
+def configs_at_n(pcfg, cfg, dev, poses, focal, image, world: int, steps: int = 10, warmup: int = 3):
+    """At N > 1: BASELINE configs[3] (Fern 504x378, 64 + 128, 1024 rays per rank, per-image bounds) in fp32 and bf16,
+    and configs[4] (Lego 800x800 bf16, 64 + 256) -- the same fused data-parallel step as the headline (weak scaling,
+    two-bucket gradient all-reduce), each timed over `steps` steps between barrier + sync pairs, max over ranks, value
+    = all ranks' rays / time. (At N = 1 the same workloads are in `extras`.)"""
+    import copy as _copy
+
+    def timed(tr, prec, pose_list, foc, img, **kw):
+        for i in range(warmup):
+            tr.step(pose_list[i % len(pose_list)][None], foc, img, **kw)
+        parallel.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            tr.step(pose_list[(warmup + i) % len(pose_list)][None], foc, img, **kw)
+        torch.cuda.synchronize()
+        parallel.barrier()
+        dt = parallel.max_over_ranks(time.perf_counter() - t0, device=dev)
+        return {"rays_per_s": round(tr.R * world * steps / dt, 1), "ms_per_step": round(1e3 * dt / steps, 3),
+                "step_mfma_frac": round(train_flops_per_ray(tr.Pc, tr.Pf) * tr.R * steps / dt / 1e12
+                                        / PEAK_TFLOPS[prec], 4)}
+
+    out = {}
+    fcfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/fern.yml")).pipeline
+    fcfg.renderer.n_pts_per_ray_fine_training = 128
+    fcfg.renderer.n_pts_per_ray_fine_evaluation = 128
+    fimg = torch.rand(1, 378, 504, 3, device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+    ffocal = torch.tensor([407.56], device=dev)
+    bounds = torch.tensor([[1.3, 5.9]])
+    out["fern_64_128_train"] = {"config": f"BASELINE configs[3] at {world} GPUs: Fern 504x378, 64 + 128, 1024 rays "
+                                          "per rank, per-image bounds"}
+    for p in ("fp32", "bf16"):
+        tr = NeRFTrainer(fcfg, precision=p, device=dev)
+        out["fern_64_128_train"][p] = timed(tr, p, poses, ffocal, fimg, near=bounds[:, :1], far=bounds[:, 1:])
+        del tr
+    c4 = _copy.deepcopy(pcfg)
+    c4.renderer.n_pts_per_ray_fine_training = 256
+    c4.renderer.n_pts_per_ray_fine_evaluation = 256
+    tr = NeRFTrainer(c4, precision="bf16", device=dev, runner_cfg=cfg.runner, train_set_size=LEGO_TRAIN_IMAGES)
+    out["lego256_bf16_train"] = {"config": f"BASELINE configs[4] at {world} GPUs: Lego 800x800 bf16, 64 + 256, 4096 "
+                                           "rays per rank", **timed(tr, "bf16", poses, focal, image)}
+    del tr
+    return out
+
+
 def psnr_leg(precision: str, steps: int, dev):
     """The `+ PSNR` half of the metric: the same fused training step (Lego config, 64 + 128, 4096 rays) trained on a
     procedural scene written in the nerf_synthetic format (tools/synthetic_scene.py: 40 train / 8 test views at
@@ -546,6 +591,9 @@ def main():
         # single-GPU characteristics (evaluation render, drop-in path, other configs, graph replay): at N > 1 every rank
         # would repeat them, and the graph capture is single-rank by design
         result["extras"] = extras(pcfg, cfg, dev, poses, focal, image, args.precision, tuple(sec))
+    elif not args.no_extras:
+        # BASELINE configs[3] / configs[4] on the same N ranks (the N-GPU half of those configs)
+        result["configs_at_n"] = configs_at_n(pcfg, cfg, dev, poses, focal, image, world)
     if rank == 0 and world == 1 and args.psnr_steps > 0:
         result["psnr"] = psnr_leg(args.precision, args.psnr_steps, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

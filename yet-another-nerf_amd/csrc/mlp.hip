@@ -1911,6 +1911,18 @@ struct DwJob {
   int a_u8;          // A stored as fp8 e4m3 of value / scale (YANERF_BF16_G8: dZ_l, dY, dZc; not dU)
   const float* a_scale;  // A's decode scale per 128-point tile
   const float* x_scale;  // X0's decode scale per 128-point tile (fp8 Y), or null
+  // fp32 (YANERF_DW_FUSE_DENSITY): this job also forms a head's weight gradient in its tiles, into that head job's slab
+  // region at ext_slab_off (the head job then has no tiles of its own):
+  //  ext 1 (intermediate_linear): density -- the dsigma row (the gradient row right after the job's 256 A rows)
+  //        against the job's own X = H_{L-1};
+  //  ext 2 (color_layer.0, its first k-tile): color_layer.2 -- ext_rows dU rows (ext_a) against the 128 rows of C
+  //        (ext_x), both staged beside the tile's own operands
+  int ext;
+  int64_t ext_slab_off;
+  const void* ext_a;
+  const void* ext_x;
+  int ext_rows, ext_ktot;
+  int gi;  // index of the job's weight gradient in the parameter list (2 * layer, ...)
 };
 constexpr int kMaxDwJobs = MAXL + 4;
 struct DwJobs {
@@ -1983,9 +1995,19 @@ constexpr int DW_STAGES = YANERF_DW_STAGES, DW_STAGE_BYTES = 512 * DW_RB;
 template <typename T> struct DwRing {
   static constexpr int STAGES = DW_STAGES, STAGE_BYTES = DW_STAGE_BYTES;
 };
+// + DW_EXT_ROWS rows per stage for a fused head (one DMA wave-instruction of A rows: the dsigma row or the dU rows,
+// then spare rows); the colour tile (128 + 128 rows) stages C's 128 rows beside them in the same 392-row stage
+constexpr int DW_EXT_ROWS = 8;
 template <> struct DwRing<float> {
-  static constexpr int STAGES = YANERF_DW32_STAGES, STAGE_BYTES = (256 + 128) * DW_RB;
+  static constexpr int STAGES = YANERF_DW32_STAGES, STAGE_BYTES = (256 + 128 + DW_EXT_ROWS) * DW_RB;
 };
+// fp32 dW: the density layer's weight gradient (one output row) formed inside the intermediate_linear tiles, which
+// stage its operand H_{L-1} anyway (an extra 16-row MFMA tile holding the dsigma row, one accumulator per wave), instead
+// of a 64-row tile with one useful row that stages H_{L-1} a second time (measured: the density and colour-output jobs
+// take 0.42 ms of the 7.6 ms fine fp32 dW). Bitwise the same density gradient (same per-accumulator point order).
+#ifndef YANERF_DW_FUSE_DENSITY
+#define YANERF_DW_FUSE_DENSITY 1
+#endif
 // points per dW stage: one K-block of the dW MFMA per staged row (x3: always one bf16 K-block, register staged)
 constexpr int X3_SPTS = 32;
 static int64_t dw_stage_pts(int prec) {
@@ -1996,15 +2018,20 @@ static int64_t dw_stage_pts(int prec) {
 __device__ __forceinline__ int dw_swz4(int row, int c) { return c ^ (((row >> 3) & 1) << 1); }  // 64-byte rows
 __device__ __forceinline__ int dw_swz(int row, int c) { return DW_CPR == 4 ? dw_swz4(row, c) : (c ^ ((row >> 1) & 7)); }
 
-template <typename T, int BN, int BK>
+template <typename T, int BN, int BK, int EXT = 0>
 __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, int64_t Npad, float* __restrict__ slab,
                                         int64_t slab_elems, char* smem) {
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
   constexpr int RSTG = DwRing<T>::STAGES, RSB = DwRing<T>::STAGE_BYTES;  // ring depth, bytes per stage
   constexpr int WN = BN / 64, WK0 = 8 / WN, WK = (BK / 16 < WK0) ? BK / 16 : WK0, KTW = BK / WK / 16;
   static_assert(KTW >= 1 && WN * WK <= 8, "dW wave tiling");
-  constexpr int ROWS = BN + BK, PW = (ROWS + 8 * DW_RPI - 1) / (8 * DW_RPI);  // DMA wave-instrs per wave per stage
-  static_assert(PW * 8 * 1024 <= RSB, "dW stage buffer");
+  // EXT: DW_EXT_ROWS head A rows after the X rows (rows XE ..), then (EXT 2) the head's 128 X rows (rows XX ..)
+  constexpr int XE = BN + BK, XX = XE + DW_EXT_ROWS, XH = EXT == 2 ? 128 : 0;
+  constexpr int ROWS = BN + BK + (EXT ? DW_EXT_ROWS + XH : 0), PW = (ROWS + 8 * DW_RPI - 1) / (8 * DW_RPI);
+  static_assert((ROWS + DW_RPI - 1) / DW_RPI * DW_RPI * DW_RB <= RSB, "dW stage buffer");
+  static_assert(EXT == 0 || (std::is_same<T, float>::value && BK == 128 && DW_CPR == 8 && DW_STAGGER &&
+                             ((EXT == 1 && BN == 256) || (EXT == 2 && BN == 128))),
+                "fused heads: fp32 256 x 128 (density) / 128 x 128 (colour output) tiles, staggered two-K-block stages");
   constexpr int KBS = DW_CPR / 4;                                             // K-blocks per stage
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2023,6 +2050,12 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
     const T* p;
     if (row < BN) {
       p = (const T*)J.A + (int64_t)(row < J.a_rows ? row : 0) * ld;  // rows past a_rows: any valid row (unused)
+    } else if (EXT == 1 && row >= XE) {
+      p = (const T*)J.A + (int64_t)(row < ROWS ? BN + (row - XE) : 0) * ld;  // dsigma (+ following rows)
+    } else if (EXT == 2 && row >= XX) {
+      p = (const T*)J.ext_x + (int64_t)(row < ROWS ? row - XX : 0) * ld;  // C
+    } else if (EXT == 2 && row >= XE) {
+      p = (const T*)J.ext_a + (int64_t)(row - XE) * ld;  // dU rows 0 .. 7
     } else {
       const int k = k0 + row - BN;
       if (k < J.x0_rows) p = (const T*)J.X0 + (int64_t)k * ld;
@@ -2034,9 +2067,12 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
   auto issue = [&](int64_t st) {
     char* dst = smem + (int)(st % RSTG) * RSB;
 #pragma unroll
-    for (int i = 0; i < PW; ++i)
-      __builtin_amdgcn_global_load_lds(src[i] + st * (KB * KBS),
-                                       (__attribute__((address_space(3))) void*)(dst + (8 * i + wave) * 1024), 16, 0, 0);
+    for (int i = 0; i < PW; ++i) {
+      // a wave-instruction whose 1 KB would reach past the stage (EXT's last one, waves >= 1) goes to the spare KB after
+      // the ring, so every wave issues PW loads per stage and the counted vmcnt waits stay uniform
+      char* d = ((8 * i + wave) * 1024 + 1024 <= RSB) ? dst + (8 * i + wave) * 1024 : smem + RSTG * RSB;
+      __builtin_amdgcn_global_load_lds(src[i] + st * (KB * KBS), (__attribute__((address_space(3))) void*)d, 16, 0, 0);
+    }
   };
   const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
   constexpr int BPT = BN * DW_CPR / DW_THREADS > 0 ? BN * DW_CPR / DW_THREADS : 1;  // bias chunks per thread
@@ -2049,11 +2085,17 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
   for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
     for (int q = 0; q < KTW; ++q) acc[nt][q] = zero;
+  [[maybe_unused]] f4 acc_e = zero;     // EXT: the head rows' accumulator (this wave's 16 columns)
+  [[maybe_unused]] float rsum_e = 0.f;  // EXT: the head biases (thread DW_CPR j + c sums chunk c of head row j)
   auto bias_rows = [&](const char* buf) {
 #pragma unroll
     for (int i = 0; i < BPT; ++i) {
       const int idx = tid + DW_THREADS * i, row = idx / DW_CPR, ch = idx % DW_CPR;
       if (row < BN) rsum[i] += hsum16<T>(*(const f4*)(buf + row * DW_RB + (ch << 4)));
+    }
+    if constexpr (EXT != 0) {
+      if (tid < DW_CPR * J.ext_rows)
+        rsum_e += hsum16<T>(*(const f4*)(buf + (XE + tid / DW_CPR) * DW_RB + ((tid % DW_CPR) << 4)));
     }
   };
   if constexpr (DW_PF && KBS == 1) {
@@ -2126,7 +2168,13 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
     // stage size.
     const bool late = wave >= 4;
     f4 a0[4], b0[KTW], a1[2][4], b1[2][KTW];
-    auto rf = [&](const char* buf, int kb, f4 (&fa)[4], f4 (&fb)[KTW]) {
+    // EXT: the extra 16-row A fragment (the head rows first; rows past the staged 8 read whatever LDS holds there --
+    // their products are never stored) and its accumulator. EXT 1: wave w multiplies it with its own column fragment
+    // QE = w / 2, so the 8 waves cover the tile's 8 column fragments once (wave w owns fragments 4 (w % 2) .. + 3);
+    // EXT 2: with column fragment w of C (rows XX + 16 w ..)
+    [[maybe_unused]] f4 e0 = zero, e1[2] = {zero, zero}, x0 = zero, x1[2] = {zero, zero};
+    const int QE = wave >> 1;
+    auto rf = [&](const char* buf, int kb, f4 (&fa)[4], f4 (&fb)[KTW], f4& fe, f4& fx) {
 #pragma unroll
       for (int q = 0; q < KTW; ++q) {
         const int row = BN + (wk * KTW + q) * 16 + li;
@@ -2137,8 +2185,16 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
         const int row = wn * 64 + 16 * nt + li;
         fa[nt] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, kb * 4 + g) << 4));
       }
+      if constexpr (EXT != 0) {
+        const int row = XE + li;
+        fe = *(const f4*)(buf + row * DW_RB + (dw_swz(row, kb * 4 + g) << 4));
+      }
+      if constexpr (EXT == 2) {
+        const int row = XX + 16 * wave + li;
+        fx = *(const f4*)(buf + row * DW_RB + (dw_swz(row, kb * 4 + g) << 4));
+      }
     };
-    auto kblock = [&](const f4 (&fa)[4], const f4 (&fb)[KTW]) {
+    auto kblock = [&](const f4 (&fa)[4], const f4 (&fb)[KTW], const f4& fe, const f4& fx) {
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
@@ -2146,6 +2202,15 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
 #pragma unroll
           for (int q = 0; q < KTW; ++q)
             acc[nt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[nt][ks], fb[q][ks], acc[nt][q], 0, 0, 0);
+      if constexpr (EXT == 1) {
+        static_assert(EXT != 1 || KTW == 4, "fused density row: four column fragments per wave");
+        const f4 bq = QE == 0 ? fb[0] : QE == 1 ? fb[1] : QE == 2 ? fb[KTW > 2 ? 2 : 0] : fb[KTW > 3 ? 3 : 0];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) acc_e = __builtin_amdgcn_mfma_f32_16x16x4f32(fe[ks], bq[ks], acc_e, 0, 0, 0);
+      } else if constexpr (EXT == 2) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) acc_e = __builtin_amdgcn_mfma_f32_16x16x4f32(fe[ks], fx[ks], acc_e, 0, 0, 0);
+      }
     };
 #pragma unroll
     for (int i = 0; i < RSTG - 1; ++i)
@@ -2165,9 +2230,9 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
     if (late && mma_wave) {
       if (st_lo < st_hi) {
         const char* buf = begin_stage(st_lo);
-        rf(buf, 0, a0, b0);
-        rf(buf, 1, a1[0], b1[0]);
-        kblock(a0, b0);
+        rf(buf, 0, a0, b0, e0, x0);
+        rf(buf, 1, a1[0], b1[0], e1[0], x1[0]);
+        kblock(a0, b0, e0, x0);
         if (do_bias) bias_rows(buf);
       }
       for (int64_t st = st_lo + 1; st < st_hi; st += 2) {
@@ -2176,26 +2241,26 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
           const int64_t sc = st + (1 - h);
           if (sc < st_hi) {
             const char* buf = begin_stage(sc);
-            rf(buf, 0, a0, b0);
-            rf(buf, 1, a1[h], b1[h]);
-            kblock(a1[h ^ 1], b1[h ^ 1]);
-            kblock(a0, b0);
+            rf(buf, 0, a0, b0, e0, x0);
+            rf(buf, 1, a1[h], b1[h], e1[h], x1[h]);
+            kblock(a1[h ^ 1], b1[h ^ 1], e1[h ^ 1], x1[h ^ 1]);
+            kblock(a0, b0, e0, x0);
             if (do_bias) bias_rows(buf);
           }
         }
       }
       if (st_hi > st_lo) {
-        if (((st_hi - 1 - st_lo) & 1) == 0) kblock(a1[0], b1[0]);
-        else kblock(a1[1], b1[1]);
+        if (((st_hi - 1 - st_lo) & 1) == 0) kblock(a1[0], b1[0], e1[0], x1[0]);
+        else kblock(a1[1], b1[1], e1[1], x1[1]);
       }
     } else {
       for (int64_t sc = st_lo; sc < st_hi; ++sc) {
         const char* buf = begin_stage(sc);
         if (mma_wave) {
-          rf(buf, 0, a0, b0);
-          rf(buf, 1, a1[0], b1[0]);
-          kblock(a0, b0);
-          kblock(a1[0], b1[0]);
+          rf(buf, 0, a0, b0, e0, x0);
+          rf(buf, 1, a1[0], b1[0], e1[0], x1[0]);
+          kblock(a0, b0, e0, x0);
+          kblock(a1[0], b1[0], e1[0], x1[0]);
         }
         if (do_bias) bias_rows(buf);
       }
@@ -2389,6 +2454,26 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
           if (n < J.a_rows && k < J.ktot) out[(int64_t)n * kv + k] = acc[nt][q][r];
         }
       }
+  }
+  if constexpr (EXT != 0) {
+    // the head rows: rows 0 .. ext_rows - 1 of the extra tile (lanes g == 0, elements 0 .. 3), this wave's column
+    // fragment (EXT 1: QE of the tile's columns; EXT 2: column fragment w of C); the head job's slab rows hold
+    // ext_ktot weights then the bias
+    float* oute = slab + (int64_t)s * slab_elems + J.ext_slab_off;
+    const int kve = J.ext_ktot + 1;
+    const int k = EXT == 1 ? k0 + (wk * KTW + (wave >> 1)) * 16 + li : 16 * wave + li;
+    if (g == 0 && k < J.ext_ktot) {
+      const float v[4] = {acc_e.x, acc_e.y, acc_e.z, acc_e.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (r < J.ext_rows) oute[(int64_t)r * kve + k] = v[r];
+    }
+    if (do_bias) {
+      float v = rsum_e;
+#pragma unroll
+      for (int o = 1; o < DW_CPR; o <<= 1) v += __shfl_xor(v, o, 64);
+      if (tid % DW_CPR == 0 && tid < DW_CPR * J.ext_rows) oute[(int64_t)(tid / DW_CPR) * kve + J.ext_ktot] = v;
+    }
   }
   if (do_bias) {
 #pragma unroll
@@ -2992,7 +3077,7 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   // x3: two buffers of three 384-row bf16 planes (144 KB); otherwise the LDS-DMA ring
   __shared__ __attribute__((aligned(16))) char smem[is_x3<T>      ? 2 * 3 * 384 * 64
                                                     : Cfg<T>::PM ? PM_STAGES * PM_STAGE_BYTES + 2 * PM_SCALES * 4
-                                                                 : DwRing<T>::STAGES * DwRing<T>::STAGE_BYTES];
+                                                                 : DwRing<T>::STAGES * DwRing<T>::STAGE_BYTES + 1024];
   // 1-D grid in job order (heaviest first); inside a job, split-major so the k-tiles sharing a dZ slab run together.
   // (An XCD-aware order -- the tiles of jobs that share a section as consecutive blocks of one XCD -- measured slower:
   // bf16 dW 1.175 -> 1.21 ms, fp32 8.23 -> 9.10 ms.)
@@ -3054,9 +3139,21 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
     // (fp32 tiles are at most dw_bkmax = 128 wide: no 256-column instantiations, whose 128 accumulators per wave would
     // set the whole kernel's VGPR count)
     static_assert(BKMAX == 128, "fp32 dW tiles");
+    if constexpr (std::is_same<T, float>::value && YANERF_DW_FUSE_DENSITY && DW_CPR == 8 && DW_STAGGER) {
+      if (bk == 128 && J.ext == 1) {
+        dw_tile<T, 256, 128, 1>(J, k0, s, S, Npad, slab, se, smem);
+        return;
+      }
+    }
     if (bk == 128) dw_tile<T, 256, 128>(J, k0, s, S, Npad, slab, se, smem);
     else dw_tile<T, 256, 64>(J, k0, s, S, Npad, slab, se, smem);
   } else if (J.bn == 128) {
+    if constexpr (std::is_same<T, float>::value && YANERF_DW_FUSE_DENSITY && DW_CPR == 8 && DW_STAGGER) {
+      if (bk == 128 && J.ext == 2 && k0 == 0) {
+        dw_tile<T, 128, 128, 2>(J, k0, s, S, Npad, slab, se, smem);
+        return;
+      }
+    }
     if (bk == 128) dw_tile<T, 128, 128>(J, k0, s, S, Npad, slab, se, smem);
     else dw_tile<T, 128, 64>(J, k0, s, S, Npad, slab, se, smem);
   } else {
@@ -3325,6 +3422,11 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
   D.slab_elems = 0;
   for_each_dw_job(L, pm, [&](const DwSpec& sp) {
     DwJob& j = D.j[D.n++];
+    j.ext = 0;
+    j.ext_slab_off = 0;
+    j.ext_a = j.ext_x = nullptr;
+    j.ext_rows = j.ext_ktot = 0;
+    j.gi = sp.gi;
     j.A = grow(sp.arow); j.a_rows = sp.a_rows;
     j.x0_u8 = j.x1_u8 = 0;
     j.a_u8 = 0;
@@ -3360,6 +3462,48 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     j.b = grads[sp.gi + 1];
   }, dir_by_ray);
   D.slab_stride = dw_slab_pad(D.slab_elems);
+  if (prec == YANERF_PREC_F32 && !pm && YANERF_DW_FUSE_DENSITY && DW_CPR == 8 && DW_STAGGER) {
+    // the density row rides in the intermediate_linear tiles (dw_tile EXT) when its gradient row directly follows the
+    // intermediate's 256 gradient rows (fp32 grad_rows: dY then dsigma) and both read the same H_{L-1} rows
+    // and the colour-output rows (dU, at most 8) ride in the first k-tile of color_layer.0 (128 rows, 128-wide tiles),
+    // which stages C's 128 rows for them beside its own operands
+    DwJob *in = nullptr, *de = nullptr, *co = nullptr, *c2 = nullptr;
+    for (int i = 0; i < D.n; ++i) {
+      if (D.j[i].gi == 2 * L.L + 0) in = &D.j[i];
+      if (D.j[i].gi == 2 * L.L + 2) de = &D.j[i];
+      if (D.j[i].gi == 2 * L.L + 4) co = &D.j[i];
+      if (D.j[i].gi == 2 * L.L + 6) c2 = &D.j[i];
+    }
+    bool changed = false;
+    if (in && de && in->bn == 256 && in->a_rows == 256 && in->ktot == 256 && in->k_tiles == 2 && !in->X1 &&
+        de->a_rows == 1 && de->X0 == in->X0 && de->ktot == in->ktot &&
+        (const char*)de->A == (const char*)in->A + 256 * ld * (int64_t)es) {
+      in->ext = 1;
+      in->ext_slab_off = de->slab_off;
+      in->ext_rows = 1;
+      in->ext_ktot = de->ktot;
+      de->k_full = de->k_tiles = 0;
+      changed = true;
+    }
+    if (co && c2 && co->bn == 128 && co->k_tiles >= 1 && co->k_full >= 1 && c2->a_rows >= 1 && c2->a_rows <= 4 &&
+        c2->ktot == 128 && !c2->X1) {
+      co->ext = 2;
+      co->ext_slab_off = c2->slab_off;
+      co->ext_a = c2->A;
+      co->ext_x = c2->X0;
+      co->ext_rows = c2->a_rows;
+      co->ext_ktot = c2->ktot;
+      c2->k_full = c2->k_tiles = 0;
+      changed = true;
+    }
+    if (changed) {
+      D.total_tiles = 0;
+      for (int i = 0; i < D.n; ++i) {
+        D.j[i].tile_base = D.total_tiles;
+        D.total_tiles += D.j[i].k_tiles;
+      }
+    }
+  }
 }
 
 static int64_t dw_slab_elems_for(const MlpLayout& L, int prec, int* total_tiles) {

@@ -1888,27 +1888,13 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
 // rows in the k-tile-0 workgroups. Partial tiles go to per-split fp32 slabs; dw_reduce sums them in split
 // order (deterministic) straight into the reference-layout gradient tensors.
 struct DwJob {
+  // (column / row counts are int16: the whole DwJobs block is a kernel argument and must stay within 4 KB)
   const void* A;  // dZ rows [a_rows][ld] (points contiguous)
-  int a_rows;
   const void* X0;  // layer input rows: segment 0 then segment 1
-  int x0_rows;
   const void* X1;
-  int x1_rows;
-  int ktot;  // x0 + x1 ; slab row length = ktot + 1 (bias column)
-  int bn;    // 256 | 128 | 64 rows per tile
-  int k_full;   // tiles of dw_bkmax(prec) columns, then (if k_tiles > k_full) one tail tile of bk_tail columns
-  int bk_tail;  // 64 | 128 | 256
-  int k_tiles, tile_base;
   int64_t slab_off;
   float* W;  // grad of weight [a_rows][ktot] (reference layout)
   float* b;  // grad of bias [a_rows]
-  // point-major operands (Cfg::PM): A / X0 / X1 are [Npad][ld] sections (A already offset to its first column);
-  // a_chunks = 16-byte chunks of A per point that hold data; the tile's column space is "virtual": X0's columns
-  // padded to x0p (a multiple of 8), then X1's (ktot_v = x0p + x1_rows); k-tiles are laid over ktot_v
-  int a_ld, a_chunks, x0_ld, x1_ld, x0p, ktot_v;
-  int w_ld;  // row stride of W: ktot, or more when trailing columns come from elsewhere (the per-ray dirPE term)
-  int x0_u8, x1_u8;  // X0 / X1 stored as fp8 e4m3 (YANERF_BF16_A8: the post-ReLU sections); a k-tile is one format
-  int a_u8;          // A stored as fp8 e4m3 of value / scale (YANERF_BF16_G8: dZ_l, dY, dZc; not dU)
   const float* a_scale;  // A's decode scale per 128-point tile
   const float* x_scale;  // X0's decode scale per 128-point tile (fp8 Y), or null
   // fp32 (YANERF_DW_FUSE_DENSITY): this job also forms a head's weight gradient in its tiles, into that head job's slab
@@ -1917,18 +1903,36 @@ struct DwJob {
   //        against the job's own X = H_{L-1};
   //  ext 2 (color_layer.0, its first k-tile): color_layer.2 -- ext_rows dU rows (ext_a) against the 128 rows of C
   //        (ext_x), both staged beside the tile's own operands
-  int ext;
   int64_t ext_slab_off;
   const void* ext_a;
   const void* ext_x;
-  int ext_rows, ext_ktot;
-  int gi;  // index of the job's weight gradient in the parameter list (2 * layer, ...)
+  int wg_base;  // first workgroup of the job in the 1-D grid
+  int16_t tS[4];  // point splits of each k-tile (equal unless the split plan balances the grid, dw_plan)
+  int16_t a_rows;
+  int16_t x0_rows;
+  int16_t x1_rows;
+  int16_t ktot;  // x0 + x1 ; slab row length = ktot + 1 (bias column)
+  int16_t bn;    // 256 | 128 | 64 rows per tile
+  int16_t k_full;   // tiles of dw_bkmax(prec) columns, then (if k_tiles > k_full) one tail tile of bk_tail columns
+  int16_t bk_tail;  // 64 | 128 | 256
+  int16_t k_tiles;
+  // point-major operands (Cfg::PM): A / X0 / X1 are [Npad][ld] sections (A already offset to its first column);
+  // a_chunks = 16-byte chunks of A per point that hold data; the tile's column space is "virtual": X0's columns
+  // padded to x0p (a multiple of 8), then X1's (ktot_v = x0p + x1_rows); k-tiles are laid over ktot_v
+  int16_t a_ld, a_chunks, x0_ld, x1_ld, x0p, ktot_v;
+  int16_t w_ld;  // row stride of W: ktot, or more when trailing columns come from elsewhere (the per-ray dirPE term)
+  int16_t x0_u8, x1_u8;  // X0 / X1 stored as fp8 e4m3 (YANERF_BF16_A8: the post-ReLU sections); a k-tile is one format
+  int16_t a_u8;          // A stored as fp8 e4m3 of value / scale (YANERF_BF16_G8: dZ_l, dY, dZc; not dU)
+  int16_t ext, ext_rows, ext_ktot;
+  int16_t gi;  // index of the job's weight gradient in the parameter list (2 * layer, ...)
 };
 constexpr int kMaxDwJobs = MAXL + 4;
 struct DwJobs {
   DwJob j[kMaxDwJobs];
   int n;
   int total_tiles;
+  int total_wg;  // workgroups of the dW launch (sum over k-tiles of their point splits)
+  int bkmax;     // dw_bkmax of the precision (the reduce maps a column to its k-tile)
   int64_t slab_elems;
   int64_t slab_stride;  // elements between two splits' slabs: slab_elems padded to a multiple of 4 (dw_slab_pad)
 };
@@ -3073,7 +3077,7 @@ __device__ __forceinline__ void run_pm(const DwJob& J, int k0, int s, int S, int
 #define YANERF_DW_XPAIR 2
 #endif
 template <typename T>
-__global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t Npad, int S, float* __restrict__ slab) {
+__global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t Npad, float* __restrict__ slab) {
   // x3: two buffers of three 384-row bf16 planes (144 KB); otherwise the LDS-DMA ring
   __shared__ __attribute__((aligned(16))) char smem[is_x3<T>      ? 2 * 3 * 384 * 64
                                                     : Cfg<T>::PM ? PM_STAGES * PM_STAGE_BYTES + 2 * PM_SCALES * 4
@@ -3081,19 +3085,34 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   // 1-D grid in job order (heaviest first); inside a job, split-major so the k-tiles sharing a dZ slab run together.
   // (An XCD-aware order -- the tiles of jobs that share a section as consecutive blocks of one XCD -- measured slower:
   // bf16 dW 1.175 -> 1.21 ms, fp32 8.23 -> 9.10 ms.)
+  // Jobs own consecutive workgroup ranges (wg_base); k-tile kt of a job runs in tS[kt] point splits.
   const int b = blockIdx.x;
   int ji = 0;
-  while (ji + 1 < jobs.n && jobs.j[ji + 1].tile_base * S <= b) ++ji;
+  while (ji + 1 < jobs.n && jobs.j[ji + 1].wg_base <= b) ++ji;
   const DwJob& J = jobs.j[ji];
-  const int local = b - J.tile_base * S;
-  int s = local / J.k_tiles, kt = local % J.k_tiles;
-  if ((YANERF_DW_XPAIR == 1 || (YANERF_DW_XPAIR == 2 && is_x3<T>)) && !Cfg<T>::PM && (S & 7) == 0 && J.k_tiles > 1) {
-    // the k-tiles of one split 8 blocks apart: blocks go to the 8 XCDs round robin, so every k-tile that stages the
-    // split's dZ rows runs on the same XCD (one L2) at about the same time (block b's XCD is b % 8 and tile_base * S
-    // is a multiple of 8)
-    const int grp = local / (8 * J.k_tiles), r = local % (8 * J.k_tiles);
-    kt = r >> 3;
-    s = grp * 8 + (r & 7);
+  const int local = b - J.wg_base;
+  bool eq = true;
+  for (int t = 1; t < J.k_tiles; ++t) eq = eq && J.tS[t] == J.tS[0];
+  int s, kt, S;
+  if (eq) {
+    // split-major inside the job, so the k-tiles sharing a dZ slab run together
+    S = J.tS[0];
+    s = local / J.k_tiles;
+    kt = local % J.k_tiles;
+    if ((YANERF_DW_XPAIR == 1 || (YANERF_DW_XPAIR == 2 && is_x3<T>)) && !Cfg<T>::PM && (S & 7) == 0 &&
+        (J.wg_base & 7) == 0 && J.k_tiles > 1) {
+      // the k-tiles of one split 8 blocks apart: blocks go to the 8 XCDs round robin, so every k-tile that stages the
+      // split's dZ rows runs on the same XCD (one L2) at about the same time (block b's XCD is b % 8)
+      const int grp = local / (8 * J.k_tiles), r = local % (8 * J.k_tiles);
+      kt = r >> 3;
+      s = grp * 8 + (r & 7);
+    }
+  } else {
+    // k-tiles with their own split counts (dw_plan balance): tile-major
+    kt = 0;
+    s = local;
+    while (kt + 1 < J.k_tiles && s >= J.tS[kt]) s -= J.tS[kt++];
+    S = J.tS[kt];
   }
   constexpr int BKMAX = dw_bkmax(prec_of<T>);
   const int k0 = kt * BKMAX;
@@ -3233,29 +3252,60 @@ __global__ void __launch_bounds__(256) dirpe_dw_final_kernel(const float* __rest
 // Sums the S split slabs in split order (deterministic): a thread owns 4 consecutive slab elements and reads them as
 // one 16-byte load per split, 8 splits' loads in flight before their adds (the slab stride is padded to a multiple of
 // 4 elements, dw_slab_pad); the sum order per element is s = 0, 1, ..., S - 1 as before.
-__global__ void dw_reduce_kernel(DwJobs jobs, int S, const float* __restrict__ slab) {
+// the point splits of slab element `local` of job J: those of the k-tile its column lies in (the bias column: k-tile 0,
+// whose workgroups form the bias gradient)
+__device__ __forceinline__ int dw_elem_splits(const DwJob& J, int64_t local, int bkmax) {
+  const int kv = J.ktot + 1;
+  const int k = (int)(local % kv);
+  if (k >= J.ktot) return J.tS[0];
+  const int kvirt = k < J.x0_rows ? k : J.x0p + (k - J.x0_rows);
+  const int t = kvirt / bkmax;
+  return J.tS[t > 3 ? 0 : t];
+}
+__global__ void dw_reduce_kernel(DwJobs jobs, const float* __restrict__ slab) {
   const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (e0 >= jobs.slab_elems) return;
   const int64_t stride = jobs.slab_stride;
-  f4 sum = f4{0.f, 0.f, 0.f, 0.f};
-  int s = 0;
-  for (; s + 8 <= S; s += 8) {
-    f4 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = *(const f4*)(slab + (int64_t)(s + u) * stride + e0);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) sum += v[u];
-  }
-  for (; s < S; ++s) sum += *(const f4*)(slab + (int64_t)s * stride + e0);
-  const float vals[4] = {sum.x, sum.y, sum.z, sum.w};
+  int jix[4], Se[4];
   int ji = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int64_t e = e0 + i;
-    if (e >= jobs.slab_elems) break;
+    jix[i] = -1;
+    Se[i] = 0;
+    if (e >= jobs.slab_elems) continue;
     while (ji + 1 < jobs.n && jobs.j[ji + 1].slab_off <= e) ++ji;
-    const DwJob& J = jobs.j[ji];
-    const int64_t local = e - J.slab_off;
+    jix[i] = ji;
+    Se[i] = dw_elem_splits(jobs.j[ji], e - jobs.j[ji].slab_off, jobs.bkmax);
+  }
+  float vals[4];
+  if (Se[1] == Se[0] && Se[2] == Se[0] && Se[3] == Se[0]) {
+    const int S = Se[0];
+    f4 sum = f4{0.f, 0.f, 0.f, 0.f};
+    int s = 0;
+    for (; s + 8 <= S; s += 8) {
+      f4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *(const f4*)(slab + (int64_t)(s + u) * stride + e0);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum += v[u];
+    }
+    for (; s < S; ++s) sum += *(const f4*)(slab + (int64_t)s * stride + e0);
+    vals[0] = sum.x; vals[1] = sum.y; vals[2] = sum.z; vals[3] = sum.w;
+  } else {
+    // a group across k-tiles with different split counts (or past the end): element by element, same order
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float t = 0.f;
+      for (int s = 0; s < Se[i]; ++s) t += slab[(int64_t)s * stride + e0 + i];
+      vals[i] = t;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (jix[i] < 0) break;
+    const DwJob& J = jobs.j[jix[i]];
+    const int64_t local = e0 + i - J.slab_off;
     const int kv = J.ktot + 1;
     const int n = (int)(local / kv), k = (int)(local % kv);
     if (k < J.ktot) J.W[(int64_t)n * J.w_ld + k] = vals[i];
@@ -3423,6 +3473,8 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
   for_each_dw_job(L, pm, [&](const DwSpec& sp) {
     DwJob& j = D.j[D.n++];
     j.ext = 0;
+    j.wg_base = 0;
+    for (int t = 0; t < 4; ++t) j.tS[t] = 0;
     j.ext_slab_off = 0;
     j.ext_a = j.ext_x = nullptr;
     j.ext_rows = j.ext_ktot = 0;
@@ -3437,8 +3489,11 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
       j.A = gsec(sp.arow, &j.a_scale);
       j.a_u8 = a_es == 1;
       const float* x1s = nullptr;  // (never scaled: the second inputs are the PE sections)
-      j.X0 = psec(sp.x0, &j.x0_u8, &j.x_scale);
-      j.X1 = psec(sp.x1, &j.x1_u8, &x1s);
+      int u0 = 0, u1 = 0;
+      j.X0 = psec(sp.x0, &u0, &j.x_scale);
+      j.X1 = psec(sp.x1, &u1, &x1s);
+      j.x0_u8 = (int16_t)u0;
+      j.x1_u8 = (int16_t)u1;
     } else {
       j.X0 = srow(sp.x0);
       j.X1 = srow(sp.x1);
@@ -3453,8 +3508,11 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     j.x0p = dw_x0p(L, pm, sp);
     j.ktot_v = j.x0p + sp.x1_rows;
     j.bn = dw_bn(sp.a_rows);
-    dw_ktiles(j.ktot_v, j.bn, prec, &j.k_full, &j.bk_tail, &j.k_tiles);
-    j.tile_base = D.total_tiles;
+    int kf = 0, bt = 0, kt = 0;
+    dw_ktiles(j.ktot_v, j.bn, prec, &kf, &bt, &kt);
+    j.k_full = (int16_t)kf;
+    j.bk_tail = (int16_t)bt;
+    j.k_tiles = (int16_t)kt;
     D.total_tiles += j.k_tiles;
     j.slab_off = D.slab_elems;
     D.slab_elems += (int64_t)sp.a_rows * (j.ktot + 1);
@@ -3498,12 +3556,94 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     }
     if (changed) {
       D.total_tiles = 0;
-      for (int i = 0; i < D.n; ++i) {
-        D.j[i].tile_base = D.total_tiles;
-        D.total_tiles += D.j[i].k_tiles;
-      }
+      for (int i = 0; i < D.n; ++i) D.total_tiles += D.j[i].k_tiles;
     }
   }
+}
+
+// Split plan (YANERF_DW_BALANCE, point-major bf16). With one split count for every k-tile, the bf16 fine dW is 448
+// workgroups of one per CU: the eight 256 x 256 tiles fill the first round and the six lighter tiles (layer 0, the
+// skip layer's PE columns, the colour layer's two tiles, the two heads: 160-384 staged bytes per point against 512)
+// a second round with 64 CUs idle -- 28 vs 23 rounds-of-work units. With YANERF_DW_BALANCE every k-tile gets splits
+// in proportion to its staged bytes per point (+ a per-point overhead), sized so the launch is YANERF_DW_BAL_ROUNDS
+// workgroups per CU of about equal work. Measured slower (profiles/r3_ab_bf16_dw_balanced_splits.jsonl, fine dW:
+// uniform 0.872-0.876 ms, balanced 2 rounds 0.886-0.896, 3 rounds 0.947-0.966, 1 round 1.21-1.22 ms): the bf16 dW
+// streams its operands at the HBM rate, so the light second round is not idle time -- the kernel is bound by its
+// bytes, and more, smaller workgroups only add prologues, epilogues and slab partials. Kept off.
+#ifndef YANERF_DW_BALANCE
+#define YANERF_DW_BALANCE 0
+#endif
+#ifndef YANERF_DW_BAL_ROUNDS
+#define YANERF_DW_BAL_ROUNDS 2
+#endif
+#ifndef YANERF_DW_BAL_SMAX
+#define YANERF_DW_BAL_SMAX 64
+#endif
+#ifndef YANERF_DW_BAL_C0
+#define YANERF_DW_BAL_C0 64
+#endif
+static bool dw_balanced(int prec) { return YANERF_DW_BALANCE && prec_pm(prec); }
+// splits the dW workspace holds (the launch's largest k-tile split count is checked against it)
+static int dw_ws_splits(int total_tiles, int64_t n_stages, int prec) {
+  const int S = dw_splits(total_tiles, n_stages, prec_pm(prec));
+  return dw_balanced(prec) && YANERF_DW_BAL_SMAX > S ? YANERF_DW_BAL_SMAX : S;
+}
+static int dw_num_cus() {
+  static int n[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (n[dev] <= 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    n[dev] = v;
+  }
+  return n[dev];
+}
+// fills every job's per-k-tile split counts (tS) and first workgroup (wg_base), and D.total_wg
+static void dw_plan(DwJobs& D, int prec, int64_t n_stages, int S) {
+  const int bkmax = dw_bkmax(prec);
+  D.bkmax = bkmax;
+  if (dw_balanced(prec)) {
+    int64_t lo = 1;
+    if (prec_pm(prec)) {  // as dw_splits: one split's fp8 gradient scales fit the tile's LDS slots
+      const int64_t cap = (int64_t)(Cfg<bf16_t>::M / PM_SPTS) * (PM_SCALES - 2);
+      lo = (n_stages + cap - 1) / cap;
+    }
+    int64_t hi = YANERF_DW_BAL_SMAX < n_stages ? YANERF_DW_BAL_SMAX : n_stages;
+    if (hi < lo) hi = lo;
+    auto cost = [&](const DwJob& j, int kt) -> int64_t {
+      const int k0 = kt * bkmax, bk = kt < j.k_full ? bkmax : j.bk_tail;
+      const bool x8 = (k0 < j.x0p) ? j.x0_u8 : j.x1_u8;
+      return (int64_t)j.a_chunks * 16 + (int64_t)bk * (x8 ? 1 : 2) + YANERF_DW_BAL_C0;
+    };
+    int64_t total = 0;
+    for (int i = 0; i < D.n; ++i)
+      for (int kt = 0; kt < D.j[i].k_tiles; ++kt) total += cost(D.j[i], kt);
+    const int64_t wgs = (int64_t)YANERF_DW_BAL_ROUNDS * dw_num_cus();
+    for (int i = 0; i < D.n; ++i)
+      for (int kt = 0; kt < D.j[i].k_tiles; ++kt) {
+        int64_t st = total > 0 ? (cost(D.j[i], kt) * wgs + total / 2) / total : 1;
+        if (st < lo) st = lo;
+        if (st > hi) st = hi;
+        D.j[i].tS[kt] = (int16_t)st;
+      }
+  } else {
+    for (int i = 0; i < D.n; ++i)
+      for (int kt = 0; kt < 4; ++kt) D.j[i].tS[kt] = (int16_t)S;
+  }
+  // heads formed inside another job's tiles (fp32 fused heads): their slab rows carry that job's splits
+  for (int i = 0; i < D.n; ++i) {
+    if (D.j[i].ext == 0) continue;
+    for (int k = 0; k < D.n; ++k)
+      if (D.j[k].k_tiles == 0 && D.j[k].slab_off == D.j[i].ext_slab_off)
+        for (int kt = 0; kt < 4; ++kt) D.j[k].tS[kt] = D.j[i].tS[D.j[i].ext == 1 ? kt : 0];
+  }
+  int wg = 0;
+  for (int i = 0; i < D.n; ++i) {
+    D.j[i].wg_base = wg;
+    for (int kt = 0; kt < D.j[i].k_tiles; ++kt) wg += D.j[i].tS[kt];
+  }
+  D.total_wg = wg;
 }
 
 static int64_t dw_slab_elems_for(const MlpLayout& L, int prec, int* total_tiles) {
@@ -3561,7 +3701,7 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   // the point splits and slab size are those of the full job set (yanerf_mlp_bwd_workspace_bytes)
   int tiles_all = 0;
   const int64_t slab_all = dw_slab_elems_for(L, prec, &tiles_all);
-  const int S = dw_splits(tiles_all, Npad / dw_stage_pts(prec), Cfg<T>::PM);
+  const int S = dw_ws_splits(tiles_all, Npad / dw_stage_pts(prec), prec);
   // the dirPE weight gradient by rays: per-ray dZc partials after the slabs, then the block partials
   constexpr int CH = dzc_chunk<T>();
   // default (1): fp32 only, where it measured -0.21 ms of 15.2 ms per Lego fine backward; bf16 and fp32x3 gained
@@ -3581,6 +3721,11 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   if (!dw && !red) return 0;
   DwJobs D;
   build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D, dir_by_ray);
+  dw_plan(D, prec, Npad / dw_stage_pts(prec), dw_splits(tiles_all, Npad / dw_stage_pts(prec), Cfg<T>::PM));
+  for (int i = 0; i < D.n; ++i)
+    for (int kt = 0; kt < D.j[i].k_tiles; ++kt)
+      YN_CHECK(D.j[i].tS[kt] >= 1 && D.j[i].tS[kt] <= S, "mlp_backward: dW job %d k-tile %d: %d splits (workspace %d)", i,
+               kt, (int)D.j[i].tS[kt], S);
   for (int i = 0; i < D.n; ++i)  // a point-major k-tile reads one X format: mixed sections must split at a tile edge
     YN_CHECK(!D.j[i].X1 || D.j[i].x0_u8 == D.j[i].x1_u8 || D.j[i].x0p % dw_bkmax(prec) == 0,
              "mlp_backward: dW job %d mixes fp8 and bf16 columns inside a tile", i);
@@ -3599,12 +3744,11 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
              "mlp_backward: dW job %d: gradient format %d does not match its %d-row tile", i, D.j[i].a_u8, D.j[i].bn);
   YN_CHECK(D.slab_stride <= dw_slab_pad(slab_all), "mlp_backward: dW slab larger than its workspace");
   if (dw) {
-    hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)(D.total_tiles * S)), dim3(DW_THREADS), 0, st, D, Npad, S,
-                       slab);
+    hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)D.total_wg), dim3(DW_THREADS), 0, st, D, Npad, slab);
     YN_LAUNCH_CHECK("mlp_backward_dw");
   }
   if (red) {
-    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((D.slab_elems + 1023) / 1024)), dim3(256), 0, st, D, S, slab);
+    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((D.slab_elems + 1023) / 1024)), dim3(256), 0, st, D, slab);
     YN_LAUNCH_CHECK("mlp_backward_reduce");
     if (dir_by_ray) {
       const int gi = 2 * L.L + 4;  // color_layer.0 weight [hdir][hid + dir_dim]
@@ -3677,7 +3821,7 @@ int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, 
   const int64_t grad_bytes = grad_t_bytes(d->n_layers, Npad, elem_size(precision), prec_pm(precision));
   int tiles = 0;
   int64_t se = dw_slab_elems_for(L, precision, &tiles);
-  int S = dw_splits(tiles, Npad / dw_stage_pts(precision), prec_pm(precision));
+  int S = dw_ws_splits(tiles, Npad / dw_stage_pts(precision), precision);
   // + the per-ray dZc partials (two slots per dZc chunk) and the dirPE block partials (rays >= chunks when used)
   const int CH = precision == YANERF_PREC_F32 ? dzc_chunk<float>()
                  : precision == YANERF_PREC_BF16 ? dzc_chunk<bf16_t>() : dzc_chunk<x3_t>();

@@ -655,6 +655,18 @@ __device__ __forceinline__ void ring_fill(ARing<T, NT>& R, const typename Cfg<T>
 // RSV (gemm_run / gemm_lds template argument): 0 no row stores, 1 a K-block's stores after its MFMAs (the forward),
 // 2 before them (the dX kernel). Measured both ways in both kernels: forward 7.58 (after) vs 7.74 ms (before); dX
 // 7.29 (after) vs 6.88 ms (before), against 7.19 ms with epilogue stores.
+// fp32 saved / gradient rows with non-temporal stores (the rows are read back by the dW kernel milliseconds and
+// gigabytes later, never from L2; the weight fragments the GEMMs stream share that L2). Measured
+// (profiles/r3_ab_fp32_save_nt.jsonl, r3_ab_x3_save_nt.jsonl): fp32 training forward 7.59-7.61 -> 7.53 ms, dX flat,
+// bitwise-equal gradients; x3 slower (dX 4.43 -> 4.56-4.60 ms), so x3 keeps plain stores.
+#ifndef YANERF_F32_SAVE_NT
+#define YANERF_F32_SAVE_NT 1
+#endif
+template <bool NT = (YANERF_F32_SAVE_NT != 0)>
+__device__ __forceinline__ void st_row_f32(const char* p, float v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, (float*)p);
+  else *(float*)p = v;
+}
 struct RowSave {
   float* base;    // saved row of the GEMM's feature 0 at the tile's first point
   uint32_t voff;  // this lane's byte offset in a 16x16 row tile (4g rows + li points)
@@ -893,10 +905,10 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const uint32_t o = vo + 16 * mt * 4;
-          *(float*)(rb + o) = b[mt].x;
-          *(float*)(rb + o + (uint32_t)rs.ldb) = b[mt].y;
-          *(float*)(rb + o + 2u * (uint32_t)rs.ldb) = b[mt].z;
-          *(float*)(rb + o + 3u * (uint32_t)rs.ldb) = b[mt].w;
+          st_row_f32(rb + o, b[mt].x);
+          st_row_f32(rb + o + (uint32_t)rs.ldb, b[mt].y);
+          st_row_f32(rb + o + 2u * (uint32_t)rs.ldb, b[mt].z);
+          st_row_f32(rb + o + 3u * (uint32_t)rs.ldb, b[mt].w);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -915,10 +927,10 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const uint32_t o = vo + 16 * mt * 4;
-          *(float*)(rb + o) = b[mt].x;
-          *(float*)(rb + o + (uint32_t)rs.ldb) = b[mt].y;
-          *(float*)(rb + o + 2u * (uint32_t)rs.ldb) = b[mt].z;
-          *(float*)(rb + o + 3u * (uint32_t)rs.ldb) = b[mt].w;
+          st_row_f32(rb + o, b[mt].x);
+          st_row_f32(rb + o + (uint32_t)rs.ldb, b[mt].y);
+          st_row_f32(rb + o + 2u * (uint32_t)rs.ldb, b[mt].z);
+          st_row_f32(rb + o + 3u * (uint32_t)rs.ldb, b[mt].w);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -1034,14 +1046,18 @@ __device__ __forceinline__ void pk_store_rows_b(typename Cfg<T>::st_t* base, uin
 template <>
 __device__ __forceinline__ void pk_store_rows_b<float>(float* base, uint32_t voff, int ldb, int so, Pk<float> p) {
   char* b = (char*)base + so + voff;
-  *(float*)b = p.v.x;
-  *(float*)(b + ldb) = p.v.y;
-  *(float*)(b + 2 * (int64_t)ldb) = p.v.z;
-  *(float*)(b + 3 * (int64_t)ldb) = p.v.w;
+  st_row_f32(b, p.v.x);
+  st_row_f32(b + ldb, p.v.y);
+  st_row_f32(b + 2 * (int64_t)ldb, p.v.z);
+  st_row_f32(b + 3 * (int64_t)ldb, p.v.w);
 }
 template <>
 __device__ __forceinline__ void pk_store_rows_b<x3_t>(float* base, uint32_t voff, int ldb, int so, Pk<x3_t> p) {
-  pk_store_rows_b<float>(base, voff, ldb, so, Pk<float>{p.v});
+  char* b = (char*)base + so + voff;
+  st_row_f32<false>(b, p.v.x);
+  st_row_f32<false>(b + ldb, p.v.y);
+  st_row_f32<false>(b + 2 * (int64_t)ldb, p.v.z);
+  st_row_f32<false>(b + 3 * (int64_t)ldb, p.v.w);
 }
 template <>
 __device__ __forceinline__ void pk_store_rows_b<bf16_t>(bf16_t* base, uint32_t voff, int ldb, int so, Pk<bf16_t> p) {

@@ -667,6 +667,12 @@ __device__ __forceinline__ void st_row_f32(const char* p, float v) {
   if constexpr (NT) __builtin_nontemporal_store(v, (float*)p);
   else *(float*)p = v;
 }
+#ifndef YANERF_F32_GSAVE_POS_FWD
+#define YANERF_F32_GSAVE_POS_FWD 1
+#endif
+#ifndef YANERF_F32_GSAVE_POS_DX
+#define YANERF_F32_GSAVE_POS_DX 2
+#endif
 struct RowSave {
   float* base;    // saved row of the GEMM's feature 0 at the tile's first point
   uint32_t voff;  // this lane's byte offset in a 16x16 row tile (4g rows + li points)
@@ -1441,7 +1447,7 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
     const bool sk = (lay.skip >> l) & 1u;
     const int kc0 = (l == 0) ? PE_COL / EPC : 0;
     const int nkb = (l == 0) ? KPE / KB : (sk ? 320 / KB : 256 / KB);
-    gemm_lds<T, NT, MT, GS ? 1 : 0>(Wt + lay.w_off[l], wpl, lay.kpad[l], nrow0, act, kc0, nkb, acc, lane, Wf + lay.b_off[l],
+    gemm_lds<T, NT, MT, GS ? YANERF_F32_GSAVE_POS_FWD : 0>(Wt + lay.w_off[l], wpl, lay.kpad[l], nrow0, act, kc0, nkb, acc, lane, Wf + lay.b_off[l],
                             &ring, hsave(l - 1));
     if (l + 1 < lay.L)
       ring_fill<T, NT>(ring, Wt + lay.w_off[l + 1], wpl, lay.kpad[l + 1], nrow0, lay.kpad[l + 1] / KB, lane);
@@ -1503,7 +1509,7 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
     }
   }
   // ---- intermediate_linear (no activation)
-  gemm_lds<T, NT, MT, GS ? 1 : 0>(Wt + lay.wint_off, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, Wf + lay.bint_off, &ring,
+  gemm_lds<T, NT, MT, GS ? YANERF_F32_GSAVE_POS_FWD : 0>(Wt + lay.wint_off, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, Wf + lay.bint_off, &ring,
                           hsave(lay.L - 1));
   const int crow0 = wave * NTC * 16;
   ARing<T, NTC> ringc;
@@ -1848,7 +1854,7 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
 #pragma unroll
     for (int w = 0; w < MW; ++w)
       bits[w] = masks[((((int64_t)hl * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane];
-    gemm_lds<T, NT, MT, GSX ? 2 : 0>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring,
+    gemm_lds<T, NT, MT, GSX ? YANERF_F32_GSAVE_POS_DX : 0>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring,
                              RowSave{(float*)(void*)(grad + (HEAD ? GR.dyx : GR.dz0 + 256LL * l) * ld + p0), soff,
                                      (int)ldb, 256 / KB, wave, WAVES});
     if (l - 1 >= 1) ring_fill<T, NT, true>(ring, Wt + lay.wt_off[l - 1], wpl, 256, nrow0, 256 / KB, lane);

@@ -667,6 +667,11 @@ __device__ __forceinline__ void st_row_f32(const char* p, float v) {
   if constexpr (NT) __builtin_nontemporal_store(v, (float*)p);
   else *(float*)p = v;
 }
+// x3 forward: the saved H rows from the next GEMM's three-plane B fragments, as the fp32 forward does. Bitwise-equal
+// gradients, not faster (training forward 5.01-5.02 vs 4.92-5.01 ms, profiles/r3_ab_x3_fwd_gsave.jsonl): kept off.
+#ifndef YANERF_X3_GSAVE
+#define YANERF_X3_GSAVE 0
+#endif
 #ifndef YANERF_F32_GSAVE_POS_FWD
 #define YANERF_F32_GSAVE_POS_FWD 1
 #endif
@@ -736,6 +741,31 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
         for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) ar[pl][nt] = *(const f4*)(wp[nt] + pl * wplane + ka * FRAG);
+      }
+      if constexpr (RSV != 0) {
+        // x3 in-GEMM saves (YANERF_X3_GSAVE): this K-block's fp32 rows rebuilt from its three bf16 planes, t0 + (t1 +
+        // t2) == v exactly (lds_put / pk_lds split v so that every residual is exact), stored after the weight refill
+        __builtin_amdgcn_sched_barrier(0);
+        if (kb < rs.nkb && kb % rs.waves == rs.wave) {
+          const char* rb = (const char*)rs.base + (int64_t)(32 * kb) * rs.ldb;
+          uint32_t vo = (uint32_t)(8 * g * rs.ldb + 4 * li);
+          asm volatile("" : "+v"(vo));
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const uint32_t o = vo + 16 * mt * 4;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+              const uint32_t w0 = __float_as_uint(b[0][mt][d]), w1 = __float_as_uint(b[1][mt][d]),
+                             w2 = __float_as_uint(b[2][mt][d]);
+              const float lo = __uint_as_float(w0 << 16) + (__uint_as_float(w1 << 16) + __uint_as_float(w2 << 16));
+              const float hi = __uint_as_float(w0 & 0xffff0000u) +
+                               (__uint_as_float(w1 & 0xffff0000u) + __uint_as_float(w2 & 0xffff0000u));
+              st_row_f32<false>(rb + o + (uint32_t)(2 * d) * (uint32_t)rs.ldb, lo);
+              st_row_f32<false>(rb + o + (uint32_t)(2 * d + 1) * (uint32_t)rs.ldb, hi);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
@@ -1437,8 +1467,9 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
   // the store's write acknowledgement too. The GEMM of layer l + 1 still reads H_l from the LDS tile, so H_l (and the
   // mask words of layer l) leave during iteration l + 1, between its GEMM and its epilogue barrier.
   uint64_t pbits[MW] = {};
-  // fp32: H_l's saved rows leave from the B fragments of the GEMM that reads H_l (YANERF_F32_GSAVE)
-  constexpr bool GS = std::is_same<T, float>::value && YANERF_F32_GSAVE && SAVE;
+  // fp32: H_l's saved rows leave from the B fragments of the GEMM that reads H_l (YANERF_F32_GSAVE); x3 likewise,
+  // rebuilt from its three planes (YANERF_X3_GSAVE)
+  constexpr bool GS = ((std::is_same<T, float>::value && YANERF_F32_GSAVE) || (is_x3<T> && YANERF_X3_GSAVE)) && SAVE;
   auto hsave = [&](int hl) {
     return RowSave{(sv && hl >= 0) ? (float*)(void*)(saved + (SR.h0 + 256LL * hl) * ld + p0) : nullptr, soff,
                    (int)ldb, (sv && hl >= 0) ? 256 / KB : 0, wave, WAVES};

@@ -684,6 +684,7 @@ struct RowSave {
   int ldb;        // row stride, bytes
   int nkb;        // K-blocks to store (the H columns; a skip layer's PE columns are saved elsewhere)
   int wave, waves;
+  int64_t blk = 0;  // (YANERF_ABLATE & 2048, timing only) byte offset of the tile's contiguous block from base
 };
 
 template <typename T, int NT, int MT, int RSV = 0>
@@ -932,7 +933,19 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
     for (int mt = 0; mt < MT; ++mt) b[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + kb * 4 + g);
     if constexpr (RSV == 2) {
       __builtin_amdgcn_sched_barrier(0);
-      if (kb < rs.nkb && kb % rs.waves == rs.wave) {
+      if ((YANERF_ABLATE & 2048) && kb < rs.nkb && kb % rs.waves == rs.wave) {
+        // timing ablation: the same stores, each wave-instruction writing 256 contiguous bytes of a per-tile block
+        const char* bb = (const char*)rs.base + rs.blk + (int64_t)kb * 4096;
+        uint32_t vo = (uint32_t)((g * 16 + li) * 4);
+        asm volatile("" : "+v"(vo));
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          st_row_f32(bb + vo + (0 * 4 + mt) * 256, b[mt].x);
+          st_row_f32(bb + vo + (1 * 4 + mt) * 256, b[mt].y);
+          st_row_f32(bb + vo + (2 * 4 + mt) * 256, b[mt].z);
+          st_row_f32(bb + vo + (3 * 4 + mt) * 256, b[mt].w);
+        }
+      } else if (kb < rs.nkb && kb % rs.waves == rs.wave) {
         // uniform 64-bit base of the K-block's 16 rows, 32-bit lane offsets (an opaque copy, so the compiler does not
         // hoist 64-bit addresses for every K-block out of the caller's layer loop)
         const char* rb = (const char*)rs.base + (int64_t)(16 * kb) * rs.ldb;
@@ -954,7 +967,19 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
     if constexpr (YANERF_PRIO == 1) __builtin_amdgcn_s_setprio(0);
     if constexpr (RSV == 1) {
       __builtin_amdgcn_sched_barrier(0);
-      if (kb < rs.nkb && kb % rs.waves == rs.wave) {
+      if ((YANERF_ABLATE & 2048) && kb < rs.nkb && kb % rs.waves == rs.wave) {
+        // timing ablation: the same stores, each wave-instruction writing 256 contiguous bytes of a per-tile block
+        const char* bb = (const char*)rs.base + rs.blk + (int64_t)kb * 4096;
+        uint32_t vo = (uint32_t)((g * 16 + li) * 4);
+        asm volatile("" : "+v"(vo));
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          st_row_f32(bb + vo + (0 * 4 + mt) * 256, b[mt].x);
+          st_row_f32(bb + vo + (1 * 4 + mt) * 256, b[mt].y);
+          st_row_f32(bb + vo + (2 * 4 + mt) * 256, b[mt].z);
+          st_row_f32(bb + vo + (3 * 4 + mt) * 256, b[mt].w);
+        }
+      } else if (kb < rs.nkb && kb % rs.waves == rs.wave) {
         // uniform 64-bit base of the K-block's 16 rows, 32-bit lane offsets (an opaque copy, so the compiler does not
         // hoist 64-bit addresses for every K-block out of the caller's layer loop)
         const char* rb = (const char*)rs.base + (int64_t)(16 * kb) * rs.ldb;
@@ -1472,7 +1497,7 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
   constexpr bool GS = ((std::is_same<T, float>::value && YANERF_F32_GSAVE) || (is_x3<T> && YANERF_X3_GSAVE)) && SAVE;
   auto hsave = [&](int hl) {
     return RowSave{(sv && hl >= 0) ? (float*)(void*)(saved + (SR.h0 + 256LL * hl) * ld + p0) : nullptr, soff,
-                   (int)ldb, (sv && hl >= 0) ? 256 / KB : 0, wave, WAVES};
+                   (int)ldb, (sv && hl >= 0) ? 256 / KB : 0, wave, WAVES, p0 * 255 * (int64_t)sizeof(ST)};
   };
   for (int l = 0; l < lay.L; ++l) {
     const bool sk = (lay.skip >> l) & 1u;
@@ -1887,7 +1912,7 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
       bits[w] = masks[((((int64_t)hl * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane];
     gemm_lds<T, NT, MT, GSX ? YANERF_F32_GSAVE_POS_DX : 0>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring,
                              RowSave{(float*)(void*)(grad + (HEAD ? GR.dyx : GR.dz0 + 256LL * l) * ld + p0), soff,
-                                     (int)ldb, 256 / KB, wave, WAVES});
+                                     (int)ldb, 256 / KB, wave, WAVES, p0 * 255 * (int64_t)sizeof(ST)});
     if (l - 1 >= 1) ring_fill<T, NT, true>(ring, Wt + lay.wt_off[l - 1], wpl, 256, nrow0, 256 / KB, lane);
     // fp8 scale sets: dZc 0, dY 1, then dZ_{L-1}, dZ_{L-2}, ... alternate from set 0
     if constexpr (PM && !(YANERF_ABLATE & 128)) {  // the GEMM's input: dY (from the heads) or dZ_l

@@ -77,6 +77,9 @@ template <typename T> struct Cfg;
 #ifndef YANERF_F32_M
 #define YANERF_F32_M 64
 #endif
+#ifndef YANERF_F32_HALVES
+#define YANERF_F32_HALVES 1
+#endif
 #ifndef YANERF_F32_WPE
 #define YANERF_F32_WPE 2
 #endif
@@ -94,7 +97,7 @@ template <typename T> struct Cfg;
 #endif
 template <> struct Cfg<float> {
   static constexpr int M = YANERF_F32_M, WAVES = 4, DXWAVES = 4, EPC = 4, KB = 16, APREF = 1, LOWREG = 0,
-                       WPE = YANERF_F32_WPE, PLANES = 1, HALVES = 1;
+                       WPE = YANERF_F32_WPE, PLANES = 1, HALVES = YANERF_F32_HALVES;
   static constexpr bool PM = false;
   typedef float lds_t;
   typedef float st_t;

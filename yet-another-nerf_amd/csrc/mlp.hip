@@ -2013,6 +2013,7 @@ struct DwJobs {
   int n;
   int total_tiles;
   int total_wg;  // workgroups of the dW launch (sum over k-tiles of their point splits)
+  int s_uniform; // the split count of every k-tile when they are all equal (dw_plan), else 0
   int bkmax;     // dw_bkmax of the precision (the reduce maps a column to its k-tile)
   int64_t slab_elems;
   int64_t slab_stride;  // elements between two splits' slabs: slab_elems padded to a multiple of 4 (dw_slab_pad)
@@ -3357,7 +3358,11 @@ __global__ void dw_reduce_kernel(DwJobs jobs, const float* __restrict__ slab) {
     if (e >= jobs.slab_elems) continue;
     while (ji + 1 < jobs.n && jobs.j[ji + 1].slab_off <= e) ++ji;
     jix[i] = ji;
-    Se[i] = dw_elem_splits(jobs.j[ji], e - jobs.j[ji].slab_off, jobs.bkmax);
+    Se[i] = jobs.s_uniform ? jobs.s_uniform : dw_elem_splits(jobs.j[ji], e - jobs.j[ji].slab_off, jobs.bkmax);
+  }
+  if (jobs.s_uniform) {  // every split count equal: past-the-end elements of the last group read in-bounds padding
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Se[i] = jobs.s_uniform;
   }
   float vals[4];
   if (Se[1] == Se[0] && Se[2] == Se[0] && Se[3] == Se[0]) {
@@ -3719,12 +3724,16 @@ static void dw_plan(DwJobs& D, int prec, int64_t n_stages, int S) {
       if (D.j[k].k_tiles == 0 && D.j[k].slab_off == D.j[i].ext_slab_off)
         for (int kt = 0; kt < 4; ++kt) D.j[k].tS[kt] = D.j[i].tS[D.j[i].ext == 1 ? kt : 0];
   }
-  int wg = 0;
+  int wg = 0, su = -1;
   for (int i = 0; i < D.n; ++i) {
     D.j[i].wg_base = wg;
-    for (int kt = 0; kt < D.j[i].k_tiles; ++kt) wg += D.j[i].tS[kt];
+    for (int kt = 0; kt < D.j[i].k_tiles; ++kt) {
+      wg += D.j[i].tS[kt];
+      su = su < 0 ? D.j[i].tS[kt] : (su == D.j[i].tS[kt] ? su : 0);
+    }
   }
   D.total_wg = wg;
+  D.s_uniform = su > 0 ? su : 0;
 }
 
 static int64_t dw_slab_elems_for(const MlpLayout& L, int prec, int* total_tiles) {

@@ -47,3 +47,18 @@ def test_kstats_by_launch_splits_modes(tmp_path):
     assert k[("k<float>", "upper mode")]["median_us"] == 8000.0 and k[("k<float>", "upper mode")]["launches"] == 4
     assert k[("k<float>", "lower mode")]["median_us"] == 2600.0
     assert k[("j", None)]["launches"] == 3
+
+
+def test_kstats_by_launch_split_ignores_stray_short_launches(tmp_path):
+    # two stray short launches of the same grid (a smaller job on the same tiles x splits) below the coarse mode: the
+    # coarse / fine jump is still the split
+    hdr = ["Kernel_Name", "Grid_Size_X", "Start_Timestamp", "End_Timestamp"]
+    rows = [["void k<float>(int)", 100, 0, 7_400_000]] * 5 + [["void k<float>(int)", 100, 0, 2_450_000]] * 5
+    rows += [["void k<float>(int)", 100, 0, 40_000]] * 2
+    _write(tmp_path / "t" / "run_kernel_trace.csv", hdr, rows)
+    out = tmp_path / "o.json"
+    subprocess.run([sys.executable, str(ROOT / "tools" / "kstats_by_launch.py"), str(tmp_path / "t"), str(out)],
+                   check=True, capture_output=True)
+    k = {x.get("mode"): x for x in json.loads(out.read_text())}
+    assert k["upper mode"]["launches"] == 5 and k["upper mode"]["median_us"] == 7400.0
+    assert k["lower mode"]["launches"] == 7

@@ -24,8 +24,10 @@ def main():
     groups = []
     for (name, grid), v in d.items():
         v = sorted(v)
-        cut = max(range(1, len(v)), key=lambda i: v[i] / max(v[i - 1], 1e-9), default=None)
-        if cut is not None and v[cut] / max(v[cut - 1], 1e-9) > 1.8 and min(cut, len(v) - cut) >= 3:
+        # (the largest jump among cuts that leave >= 3 launches on each side: a few stray short launches below the
+        # coarse pass must not hide the coarse / fine jump)
+        cut = max(range(3, len(v) - 2), key=lambda i: v[i] / max(v[i - 1], 1e-9), default=None)
+        if cut is not None and v[cut] / max(v[cut - 1], 1e-9) > 1.8:
             groups += [(name, grid, v[:cut], "lower mode"), (name, grid, v[cut:], "upper mode")]
         else:
             groups.append((name, grid, v, None))

@@ -642,6 +642,10 @@ def test_lego256_mlp_gradients_vs_oracle(pkg, precision):
         else:
             assert rel <= 5e-3, name
             assert np.abs(v - r).max() <= 2e-2 * np.abs(r).max(), name
+            if name.startswith(("density_layer.", "color_layer.2.")):
+                # the heads' weight gradients (fp32: formed inside the intermediate / colour tiles of the dW kernel,
+                # YANERF_DW_FUSE_DENSITY): a ReLU flip moves an H_7 / C value that is itself ~0, so these stay strict
+                assert rel <= 1e-4, (name, rel)
 
 
 @pytest.mark.parametrize("precision", FP32_MODES + ["bf16"])

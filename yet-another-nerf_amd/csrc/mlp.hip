@@ -675,9 +675,6 @@ __device__ __forceinline__ void st_row_f32(const char* p, float v) {
 #ifndef YANERF_X3_GSAVE
 #define YANERF_X3_GSAVE 0
 #endif
-#ifndef YANERF_F32_GSAVE_ROT
-#define YANERF_F32_GSAVE_ROT 0
-#endif
 #ifndef YANERF_F32_GSAVE_POS_FWD
 #define YANERF_F32_GSAVE_POS_FWD 1
 #endif
@@ -925,73 +922,6 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
     }
     if (kb < nkb) half(kb, a0, a1);
     return;
-  }
-  if constexpr (RSV == 1 && YANERF_F32_GSAVE_ROT) {
-    // fp32 forward, in-GEMM saves at a STATIC loop position (YANERF_F32_GSAVE_ROT): wave w walks the stored K-blocks
-    // in the order w, w + 1, ..., rs.nkb - 1, 0, ..., w - 1 (then any unstored ones, e.g. the skip layer's PE
-    // columns), so its own blocks (kb = w mod 4) fall on every fourth step of a 4-way unrolled loop. With the stores
-    // under a runtime `kb % waves == wave` test, the compiler merges the storing and non-storing paths at the loop
-    // head and waits there with vmcnt(0) -- for the weight loads AND the stores just issued; with the stores' steps
-    // known statically it waits only for the loads issued before them. (The accumulation order over K-blocks is
-    // rotated per wave: a different but deterministic fp32 summation order.)
-    if (rs.nkb > 0 && rs.waves == 4 && (nkb & 3) == 0 && (rs.nkb & 3) == 0 && rs.nkb <= nkb) {
-      const int w = rs.wave;
-      auto kidx = [&](int i) {
-        if (i >= rs.nkb) return i;
-        const int k = i + w;
-        return k >= rs.nkb ? k - rs.nkb : k;
-      };
-      f4 a[NT];
-      {
-        const int k0 = kidx(0);
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) a[nt] = *(const f4*)(wp[nt] + k0 * FRAG);
-      }
-      auto step = [&](int i, auto store) {
-        const int k = kidx(i);
-        const int kn = kidx(i + 1 < nkb ? i + 1 : i);
-        f4 an[NT];
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) an[nt] = *(const f4*)(wp[nt] + kn * FRAG);
-        f4 b[MT];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) b[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + k * 4 + g);
-        mma_grid<T, NT, MT>(a, b, acc);
-        if constexpr (decltype(store)::value) {
-          __builtin_amdgcn_sched_barrier(0);
-          const char* rb = (const char*)rs.base + (int64_t)(16 * k) * rs.ldb;
-          uint32_t vo = rs.voff;
-          asm volatile("" : "+v"(vo));
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const uint32_t o = vo + 16 * mt * 4;
-            st_row_f32(rb + o, b[mt].x);
-            st_row_f32(rb + o + (uint32_t)rs.ldb, b[mt].y);
-            st_row_f32(rb + o + 2u * (uint32_t)rs.ldb, b[mt].z);
-            st_row_f32(rb + o + 3u * (uint32_t)rs.ldb, b[mt].w);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) a[nt] = an[nt];
-      };
-      using ST1 = std::integral_constant<bool, true>;
-      using SF = std::integral_constant<bool, false>;
-      int i = 0;
-      for (; i < rs.nkb; i += 4) {
-        step(i, ST1{});
-        step(i + 1, SF{});
-        step(i + 2, SF{});
-        step(i + 3, SF{});
-      }
-      for (; i < nkb; i += 4) {
-        step(i, SF{});
-        step(i + 1, SF{});
-        step(i + 2, SF{});
-        step(i + 3, SF{});
-      }
-      return;
-    }
   }
   f4 a[NT];
 #pragma unroll

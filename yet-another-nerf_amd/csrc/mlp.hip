@@ -675,6 +675,15 @@ __device__ __forceinline__ void st_row_f32(const char* p, float v) {
 #ifndef YANERF_X3_GSAVE
 #define YANERF_X3_GSAVE 0
 #endif
+// fp32 GEMM loop: the copy of the prefetched weight fragments into the current set pinned after the K-block's MFMAs
+// (1: every GEMM, 2: the GEMMs without in-GEMM row stores). Left free, the compiler interleaves the 16 copies with the
+// MFMAs and so waits for the next block's loads a quarter of the way into the current one. Measured
+// (profiles/r3_ab_fp32_latecopy_all.jsonl, r3_ab_fp32_latecopy_storefree.jsonl; bitwise equal): inference forward
+// 7.04-7.09 -> 6.93-6.98 ms; the training forward is unchanged (its row stores already sit between the MFMAs and the
+// copies) and the dX slower with it (6.90 -> 7.19 ms), so 2.
+#ifndef YANERF_F32_LATECOPY
+#define YANERF_F32_LATECOPY 2
+#endif
 #ifndef YANERF_F32_GSAVE_POS_FWD
 #define YANERF_F32_GSAVE_POS_FWD 1
 #endif
@@ -999,6 +1008,7 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (YANERF_F32_LATECOPY == 1 || (YANERF_F32_LATECOPY == 2 && RSV == 0)) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) a[nt] = an[nt];
   }

@@ -681,6 +681,17 @@ __device__ __forceinline__ void st_row_f32(const char* p, float v) {
 // (profiles/r3_ab_fp32_latecopy_all.jsonl, r3_ab_fp32_latecopy_storefree.jsonl; bitwise equal): inference forward
 // 7.04-7.09 -> 6.93-6.98 ms; the training forward is unchanged (its row stores already sit between the MFMAs and the
 // copies) and the dX slower with it (6.90 -> 7.19 ms), so 2.
+// training / inference forward as separate instantiations with the saves' presence known at compile time (STAT; else
+// the kernel tests the saved pointer at run time). With the run-time test the compiler merges the saving and
+// non-saving paths, and at the next GEMM's first weight use waits with vmcnt(0) -- for the previous epilogue's saved-row
+// and mask stores too -- instead of counting past them. Measured (profiles/r3_ab_static_save_instantiation.jsonl,
+// bitwise equal): x3 training forward 4.97-5.00 -> 4.86-4.88 ms, fp32 7.57 -> 7.51-7.54 ms.
+#ifndef YANERF_X3_STAT
+#define YANERF_X3_STAT 1
+#endif
+#ifndef YANERF_F32_STAT
+#define YANERF_F32_STAT 1
+#endif
 #ifndef YANERF_F32_LATECOPY
 #define YANERF_F32_LATECOPY 2
 #endif
@@ -1469,7 +1480,8 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
   // bf16 has separate training / inference instantiations (branch-free epilogues); fp32 / x3 keep one kernel that
   // tests the saved pointer at run time (with a branch-free epilogue the compiler interleaves it into the GEMM loop
   // and the fp32 MFMA schedule measured slower: training forward 7.7 -> 8.3 ms)
-  constexpr bool STAT = sizeof(T) == 2 && !is_x3<T>;
+  constexpr bool STAT = (sizeof(T) == 2 && !is_x3<T>) || (is_x3<T> && YANERF_X3_STAT) ||
+                        (std::is_same<T, float>::value && YANERF_F32_STAT);
   const bool sv = STAT ? SAVE : saved != nullptr;
   const int64_t wpl = lay.t_plane;
   const SavedRows SR = saved_rows(lay.L);
@@ -3775,7 +3787,8 @@ static int launch_fwd(const MlpLayout& L, int prec, const void* packed, const fl
   dim3 grid((unsigned)(Npad / (Cfg<T>::M * Cfg<T>::HALVES))), block(Cfg<T>::HALVES * Cfg<T>::WAVES * 64);
   uint64_t* masks = saved ? (uint64_t*)((char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM)) : nullptr;
   // bf16 and (with the in-GEMM saves) fp32 inference run the instantiation without the save code
-  constexpr bool SPLIT = std::is_same<T, bf16_t>::value || (std::is_same<T, float>::value && YANERF_F32_GSAVE);
+  constexpr bool SPLIT = std::is_same<T, bf16_t>::value || (std::is_same<T, float>::value && YANERF_F32_GSAVE) ||
+                         (is_x3<T> && YANERF_X3_STAT);
   if (saved || !SPLIT)
     hipLaunchKernelGGL((mlp_fwd_kernel<T, true>), grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, (ST*)saved,
                        saved ? masks : nullptr, Npad);

@@ -305,13 +305,20 @@ def gen_render_eval(out):
 def gen_train_step(out):
     n_rays = 48
     pcfg = lego_pipeline_cfg(n_rays=n_rays)
-    pipe = PIPELINES.build(pcfg)
-    load_pipeline_weights(pipe, (21, 22))
-    pipe.train()
     pose = torch.from_numpy(synthetic_pose(-60.0, -20.0, 4.0))[None]
     focal = torch.tensor([1111.1111])
     g = torch.Generator().manual_seed(8)
     img = torch.rand(1, 800, 800, 3, generator=g)
+    out["train_step_lego"] = record_train_step(pcfg, (21, 22), pose, focal, img, n_rays, torch_seed=10)
+
+
+def record_train_step(pcfg, seeds, pose, focal, img, n_rays, torch_seed, min_depth=None, max_depth=None):
+    """One reference training step (NeRFPipeline TRAINING forward + objective backward) with every random draw, the
+    refiner's inputs / outputs, both MLPs' ReLU decisions, the losses, the rasterized MC outputs and the parameter
+    gradients recorded."""
+    pipe = PIPELINES.build(pcfg)
+    load_pipeline_weights(pipe, seeds)
+    pipe.train()
     rec = Recorder()
     # the refiner's input weights and output depths (RayPointRefiner.forward, renderers/utils.py:48-69; the fine pass
     # runs at these depths, multipass_emission_absorpsion_renderer.py:107-114): recorded through a pass-through wrapper
@@ -334,10 +341,12 @@ def gen_train_step(out):
         for key, mod in mods:
             hooks.append(mod.register_forward_hook(
                 lambda m, i, o, key=key: relu.__setitem__(key, (o.detach() > 0).reshape(-1, o.shape[-1]).numpy())))
-    torch.manual_seed(10)
+    torch.manual_seed(torch_seed)
+    bounds = {} if min_depth is None else dict(min_depth=min_depth, max_depth=max_depth)
     try:
         with rec.capture():
-            preds = pipe(poses=pose, focal_lengths=focal, image_rgb=img, evaluation_mode=EvaluationMode.TRAINING)
+            preds = pipe(poses=pose, focal_lengths=focal, image_rgb=img, evaluation_mode=EvaluationMode.TRAINING,
+                         **bounds)
     finally:
         RayPointRefiner.forward = orig_fwd
         for h in hooks:
@@ -345,13 +354,21 @@ def gen_train_step(out):
     preds["objective"].mean().backward()
     ids = rec.take("multinomial")[0].numpy().astype(np.int64)
     assert len(refined) == 1
-    d = dict(pose=np32(pose), focal=np32(focal), seeds=np.array([21, 22]), n_rays=np.int64(n_rays),
+    d = dict(pose=np32(pose), focal=np32(focal), seeds=np.array(list(seeds)), n_rays=np.int64(n_rays),
              pixel_ids=ids, gt_rgb=np32(img.reshape(1, -1, 3)[0, ids[0]]),
              jitter_u=np32(rec.take("rand_like")[0]),
-             noise_coarse=np32(rec.take("randn_like")[0]), noise_fine=np32(rec.take("randn_like")[1]),
              pdf_u=np32(rec.take("rand")[0]),
              coarse_weights=np32(refined[0][0]).reshape(n_rays, -1), z_fine=np32(refined[0][1]).reshape(n_rays, -1))
+    noise = rec.take("randn_like")
+    if noise:
+        d["noise_coarse"], d["noise_fine"] = np32(noise[0]), np32(noise[1])
+    if min_depth is not None:
+        d["min_depth"], d["max_depth"] = np32(min_depth), np32(max_depth)
     for k in ("objective", "loss_rgb_mse", "loss_prev_stage_rgb_mse", "loss_rgb_huber"):
+        d[k] = np32(preds[k])
+    # the Monte-Carlo rays splatted onto full-size images (output_rasterized_mc: nerf_pipeline.py:196-201 ->
+    # _rasterize_mc_samples -> scatter_rays_to_image, pipelines/utils.py:299-323), mostly zeros (compressed)
+    for k in ("rendered_images", "rendered_depths", "rendered_alpha_masks"):
         d[k] = np32(preds[k])
     for k in range(len(pipe.implicit_functions)):  # bit-packed along the feature axis (np.packbits, big-endian)
         d[f"relu{k}:trunk"] = np.stack([np.packbits(relu[f"{k}:trunk{li}"], axis=-1) for li in range(8)])
@@ -367,7 +384,159 @@ def gen_train_step(out):
                 idx = rng.choice(gr.size, size=256, replace=False)
                 d[f"gradidx{i}:{name}"] = idx.astype(np.int64)
                 d[f"gradval{i}:{name}"] = gr.reshape(-1)[idx]
-    out["train_step_lego"] = d
+    return d
+
+
+# BASELINE configs[3]: the reference's own Fern config (fern.yml) at 64 + 64 and BASELINE's 64 + 128, with LLFF-style
+# per-image depth bounds as (B, 1) tensors (llff_dataset.py items; ray_sampler.py:280-283 averages them with .item())
+FERN_FOCAL, FERN_NEAR, FERN_FAR = 407.6, 1.3125, 7.25
+
+
+def fern_pipeline_cfg(n_fine, n_rays=1024):
+    cfg = Config.fromfile(str(REF / "configs/nerf/fern.yml"))
+    p = cfg.pipeline
+    p.renderer.n_pts_per_ray_fine_training = n_fine
+    p.renderer.n_pts_per_ray_fine_evaluation = n_fine
+    p.ray_sampler.n_rays_per_image_sampled_from_mask = n_rays
+    return p
+
+
+def record_eval_render(pipe, pose, focal, H, W, **bounds):
+    """The reference's two-pass EVALUATION render through its renderer, with the per-stage outputs: coarse features /
+    depths / weights, the refined depths (RayPointRefiner, recorded through a pass-through wrapper) and the fine
+    features / depths."""
+    refined = []
+    orig_fwd = RayPointRefiner.forward
+
+    def rec_fwd(self, origins, directions, lengths, xys, ray_weights):
+        rb = orig_fwd(self, origins, directions, lengths, xys, ray_weights)
+        refined.append(rb.lengths.detach().clone())
+        return rb
+
+    RayPointRefiner.forward = rec_fwd
+    try:
+        rb = pipe.ray_sampler(pose, focal, evaluation_mode=EvaluationMode.EVALUATION, image_height=H, image_width=W,
+                              **bounds)
+        with torch.no_grad():
+            ro = pipe.renderer(*rb, bg_color=None, implicit_functions=pipe.implicit_functions,
+                               evaluation_mode=EvaluationMode.EVALUATION)
+    finally:
+        RayPointRefiner.forward = orig_fwd
+    R = H * W
+    pv = ro.prev_stage
+    return dict(lengths=np32(rb.lengths).reshape(R, -1), coarse_features=np32(pv.features).reshape(R, -1),
+                coarse_depths=np32(pv.depths).reshape(R), coarse_weights=np32(pv.aux["weights"]).reshape(R, -1),
+                z_fine=np32(refined[0]).reshape(R, -1), fine_features=np32(ro.features).reshape(R, -1),
+                fine_depths=np32(ro.depths).reshape(R))
+
+
+def gen_render_fern(out):
+    from scene import forward_pose
+    near, far = torch.tensor([[FERN_NEAR]]), torch.tensor([[FERN_FAR]])
+    for n_fine in (64, 128):
+        pipe = PIPELINES.build(fern_pipeline_cfg(n_fine))
+        load_pipeline_weights(pipe, (41, 42))
+        pipe.eval()
+        pose = torch.from_numpy(forward_pose())[None]
+        focal = torch.tensor([FERN_FOCAL])
+        d = record_eval_render(pipe, pose, focal, 9, 12, min_depth=near, max_depth=far)
+        d.update(pose=np32(pose), focal=np32(focal), H=np.int64(9), W=np.int64(12), seeds=np.array([41, 42]),
+                 n_fine=np.int64(n_fine), min_depth=np32(near), max_depth=np32(far))
+        out[f"render_fern_{n_fine}"] = d
+
+
+def gen_train_step_fern(out):
+    from scene import forward_pose
+    near, far = torch.tensor([[FERN_NEAR]]), torch.tensor([[FERN_FAR]])
+    for n_fine in (64, 128):
+        n_rays = 64
+        pose = torch.from_numpy(forward_pose(0.03))[None]
+        focal = torch.tensor([FERN_FOCAL])
+        g = torch.Generator().manual_seed(15 + n_fine)
+        img = torch.rand(1, 378, 504, 3, generator=g)
+        out[f"train_step_fern_{n_fine}"] = record_train_step(fern_pipeline_cfg(n_fine, n_rays), (51, 52), pose, focal,
+                                                             img, n_rays, torch_seed=16 + n_fine, min_depth=near,
+                                                             max_depth=far)
+
+
+def gen_sensitivity(out):
+    """How far the REFERENCE's own two-pass render moves under equally valid fp32 evaluations of its coarse stage: the
+    Lego 16 x 16 evaluation render (render_eval_lego's config) and the Fern 9 x 12 renders (render_fern_*), each
+    re-run (a) in float64 end to end (torch default dtype float64, the modules in double: the reference's algorithm
+    without fp32 rounding), (b) with every result of torch.exp moved one ulp up or down (random signs: another correctly
+    rounded exp, as in the capping function 1 - exp(-x)), (c) with every coarse parameter moved one ulp, (d) with the
+    K-sums of every Linear layer split into 2 / 3 / 4 / 8 partial sums (another valid fp32 summation order). Per ray:
+    the largest move of its refined depths and fine RGB over (b)-(d), and the float64 depths / RGB. sample_pdf's
+    conditioning (renderers/utils.py:72-158: a pdf of ~1e-5 where the coarse weights hold no mass, at the `denom < eps`
+    branch) turns such ulp-level differences of the coarse weights into moves of fine samples up to a bin width; the
+    parity tests compare the set of rays whose refined depths differ between this build and the reference with the set
+    of rays the reference itself moves this way (sensitive = float64 move or any (b)-(d) move above 2e-5)."""
+    import torch.nn.functional as Fn
+    from scene import forward_pose
+    cases = [("lego", lego_pipeline_cfg(), (11, 12), torch.from_numpy(synthetic_pose(30.0, -30.0, 4.0))[None],
+              torch.tensor([1111.1111]), 16, 16, {})]
+    for n_fine in (64, 128):
+        cases.append((f"fern_{n_fine}", fern_pipeline_cfg(n_fine), (41, 42), torch.from_numpy(forward_pose())[None],
+                      torch.tensor([FERN_FOCAL]), 9, 12,
+                      dict(min_depth=torch.tensor([[FERN_NEAR]]), max_depth=torch.tensor([[FERN_FAR]]))))
+
+    def ulp(a, rng):
+        up = rng.integers(0, 2, size=a.shape).astype(bool)
+        return np.where(up, np.nextafter(a, np.float32(np.inf)), np.nextafter(a, np.float32(-np.inf))).astype(np.float32)
+
+    texp, flin = torch.exp, Fn.linear
+    for name, pcfg, seeds, pose, focal, H, W, bounds in cases:
+        pipe = PIPELINES.build(pcfg)
+        load_pipeline_weights(pipe, seeds)
+        pipe.eval()
+        base = record_eval_render(pipe, pose, focal, H, W, **bounds)
+        R = H * W
+        dz, drgb = np.zeros(R), np.zeros(R)
+
+        def note(r):
+            np.maximum(dz, np.abs(r["z_fine"].astype(np.float64) - base["z_fine"]).max(-1), out=dz)
+            np.maximum(drgb, np.abs(r["fine_features"].astype(np.float64) - base["fine_features"]).max(-1), out=drgb)
+
+        coarse = pipe.implicit_functions[0]._fn
+        orig = {k: v.detach().clone() for k, v in coarse.state_dict().items()}
+        for trial in range(8):  # (b) exp one ulp off
+            rng = np.random.Generator(np.random.PCG64(1000 + trial))
+            torch.exp = lambda x, *a, rng=rng, **k: torch.from_numpy(ulp(texp(x, *a, **k).numpy(), rng))
+            try:
+                note(record_eval_render(pipe, pose, focal, H, W, **bounds))
+            finally:
+                torch.exp = texp
+        for trial in range(8):  # (c) coarse parameters one ulp off
+            rng = np.random.Generator(np.random.PCG64(2000 + trial))
+            coarse.load_state_dict({k: torch.from_numpy(ulp(v.numpy(), rng)) for k, v in orig.items()})
+            note(record_eval_render(pipe, pose, focal, H, W, **bounds))
+        coarse.load_state_dict(orig)
+        for nsplit in (2, 3, 4, 8):  # (d) Linear K-sums in nsplit partial sums
+            def lin(x, w, bias=None, nsplit=nsplit):
+                cuts = np.linspace(0, w.shape[1], nsplit + 1).astype(int)
+                y = None
+                for a0, a1 in zip(cuts[:-1], cuts[1:]):
+                    part = flin(x[..., a0:a1], w[:, a0:a1])
+                    y = part if y is None else y + part
+                return y if bias is None else y + bias
+            Fn.linear = lin
+            try:
+                note(record_eval_render(pipe, pose, focal, H, W, **bounds))
+            finally:
+                Fn.linear = flin
+        # (a) float64
+        torch.set_default_dtype(torch.float64)
+        pipe.double()
+        try:
+            r64 = record_eval_render(pipe, pose.double(), focal.double(), H, W,
+                                     **{k: v.double() for k, v in bounds.items()})
+        finally:
+            torch.set_default_dtype(torch.float32)
+            pipe.float()
+        out[f"sensitivity_{name}"] = dict(
+            trials=np.int64(20), max_z_move=dz.astype(np.float32), max_rgb_move=drgb.astype(np.float32),
+            z_fine=base["z_fine"], fine_features=base["fine_features"], z_fine_f64=r64["z_fine"].astype(np.float64),
+            fine_features_f64=r64["fine_features"].astype(np.float64))
 
 
 def gen_zero_outputer(out):
@@ -603,7 +772,7 @@ def gen_iter_runner(out):
 
 GENERATORS = (gen_harmonic, gen_raysampler, gen_mlp, gen_raymarcher, gen_sample_pdf, gen_render_eval,
               gen_train_step, gen_zero_outputer, gen_init_checksums, gen_pipeline_state, gen_lr_schedule,
-              gen_raysampler_masked, gen_iter_runner)
+              gen_raysampler_masked, gen_iter_runner, gen_render_fern, gen_train_step_fern, gen_sensitivity)
 
 
 def main():

@@ -27,3 +27,12 @@ def synthetic_pose(theta_deg: float, phi_deg: float, radius: float) -> np.ndarra
     c2w = np.array([[-1, 0, 0, 0], [0, 0, 1, 0], [0, 1, 0, 0], [0, 0, 0, 1]], dtype=np.float64) @ c2w
     flip = np.diag([1.0, -1.0, -1.0, 1.0])
     return (c2w @ flip)[:3, :4].astype(np.float32)
+
+
+def forward_pose(shift: float = 0.0) -> np.ndarray:
+    """A forward-facing LLFF-style camera (identity rotation, looking down -z) used by the Fern-config goldens and
+    tests: c2w [3, 4] with the camera at (0.1 + shift, -0.05, 4)."""
+    pose = np.eye(4, dtype=np.float32)[:3].copy()
+    pose[:, 3] = [0.1 + shift, -0.05, 4.0]
+    return pose
+

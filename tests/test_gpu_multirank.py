@@ -198,6 +198,48 @@ def test_trainer_gradient_exchange_two_ranks():
         assert a[k]["lr"] == lr_at(runner, k, world_size=2) == b[k]["lr"]
 
 
+def _exchange_worker(rank, world, port, q, precision):
+    """Three fused training steps per rank under each gradient exchange ("bucketed": one all-reduce per model, the
+    coarse one overlapped with the fine backward; "single": one all-reduce of the whole flat gradient after both
+    backwards), from the same seed and rank-specific images; records the parameters and Adam moments after the steps."""
+    _init_worker(rank, world, port)
+    from scene import synthetic_pose
+    from yanerf_amd import parallel
+    from yanerf_amd.train import NeRFTrainer
+    from yanerf_amd.utils.config import Config
+    import yanerf_boot
+    cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml"))
+    g = torch.Generator().manual_seed(200 + rank)
+    img = torch.rand(1, 800, 800, 3, generator=g).to("cuda:0")
+    out = {}
+    for exch in ("bucketed", "single"):
+        tr = NeRFTrainer(cfg.pipeline, precision=precision, device="cuda:0", n_rays=256, runner_cfg=cfg.runner,
+                         seed=42, grad_exchange=exch)
+        for k in range(3):
+            pose = torch.from_numpy(synthetic_pose(25.0 * k + 90.0 * rank, -30.0, 4.0)).float()[None].to("cuda:0")
+            tr.step(pose, torch.tensor([1111.111], device="cuda:0"), img)
+        torch.cuda.synchronize()
+        out[exch] = dict(params=tr.flat.data.detach().cpu().clone(), m=tr.exp_avg.detach().cpu().clone(),
+                         v=tr.exp_avg_sq.detach().cpu().clone())
+        del tr
+    q.put(_by_value((rank, out)))
+    parallel.barrier()
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_bucketed_and_single_exchange_give_identical_parameters(precision):
+    """configs[2]'s exchange (scripts/run.py:162-166 DDP semantics) in both of the trainer's schedules: after three
+    steps on two ranks the bucketed (overlapped) and the single all-reduce give bit-identical parameters and Adam
+    moments, on both ranks, in fp32 and bf16 -- the bucketing changes when the sums run, not what they sum."""
+    res = _spawn(_exchange_worker, 2, extra=(precision,))
+    (_, a), (_, b) = res
+    for key in ("params", "m", "v"):
+        assert torch.equal(a["bucketed"][key], a["single"][key]), key
+        assert torch.equal(a["bucketed"][key], b["bucketed"][key]), key
+        assert torch.equal(b["bucketed"][key], b["single"][key]), key
+
+
 def _ddp_worker(rank, world, port, q, golden_dir):
     """The drop-in path as scripts/run.py:162-166 runs it: the registry NeRFPipeline wrapped in
     DistributedDataParallel(find_unused_parameters=True); one step on rank-specific data with injected draws, and the

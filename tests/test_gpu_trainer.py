@@ -464,3 +464,49 @@ def test_graph_render_equals_eager_render(precision):
         if k == 2:  # an eager render of another chunk size replaces the eager buffer cache; the graph keeps its own
             tr.render(poses[0], focal, 40, 40, chunk=512)
     assert tr._render_graph is not None and tr._render_graph[0] == (H, W, None, None, 4096)
+
+
+def test_graph_replayed_steps_follow_per_image_bounds():
+    """A captured step reads its depth range from a static device buffer: replay_step(near=, far=) with LLFF-style
+    per-image bound tensors (device and host) gives bit for bit the eager steps fed the same bounds, and a replay
+    without bounds keeps the previous replay's range (ray_sampler.py:280-283 averages the bounds)."""
+    from scene import synthetic_pose
+    from yanerf_amd.train import NeRFTrainer
+    cfg = lego_cfg()
+    trs = [NeRFTrainer(cfg.pipeline, precision="fp32", device=DEV, n_rays=256, seed=9) for _ in range(2)]
+    img = torch.rand(1, 800, 800, 3, device=DEV, generator=torch.Generator(device=DEV).manual_seed(6))
+    poses = [torch.from_numpy(synthetic_pose(25.0 * k, -30.0, 4.0)).float()[None].to(DEV) for k in range(5)]
+    focal = torch.tensor([1111.111], device=DEV)
+    bounds = [(torch.tensor([[1.5]], device=DEV), torch.tensor([[5.5]], device=DEV)),
+              (torch.tensor([[2.5]]), torch.tensor([[4.0]])),  # host tensors
+              (None, None), (2.2, 6.1)]
+    eager, graph = trs
+    graph.step(poses[0], focal, img)
+    eager.step(poses[0], focal, img)
+    graph.capture_step(poses[1], focal, img)
+    prev = (None, None)
+    for k, (nr, fr) in enumerate(bounds):
+        use = prev if nr is None else (nr, fr)
+        a = eager.step(poses[k + 1], focal, img, near=use[0], far=use[1])
+        b = graph.replay_step(poses[k + 1], focal, near=nr, far=fr)
+        torch.cuda.synchronize()
+        assert torch.equal(a["sq_fine"], b["sq_fine"]) and torch.equal(a["sq_coarse"], b["sq_coarse"]), k
+        prev = use
+    assert torch.equal(eager.flat.data, graph.flat.data)
+
+
+def test_graph_render_advances_the_training_stream_like_render():
+    """render_graph advances the trainer's Philox counter by what an eager render() draws, so training steps after an
+    evaluation draw the same pixels, jitter and noise whichever render path ran."""
+    from scene import synthetic_pose
+    from yanerf_amd.train import NeRFTrainer
+    cfg = lego_cfg()
+    trs = [NeRFTrainer(cfg.pipeline, precision="fp32", device=DEV, n_rays=256, seed=4) for _ in range(2)]
+    focal = torch.tensor([1111.111 * 64 / 800], device=DEV)
+    pose = torch.from_numpy(synthetic_pose(10.0, -30.0, 4.0)).float()[None].to(DEV)
+    eager, graph = trs
+    for _ in range(3):
+        eager.render(pose, focal, 64, 64, chunk=1024)
+        graph.render_graph(pose, focal, 64, 64, chunk=1024)
+    assert eager.rng.get_state() == graph.rng.get_state()
+

@@ -74,6 +74,12 @@ def main(R=4096, P=192, reps=10):
         torch.cuda.synchronize()
         import hashlib
         res[f"{prec}_grad_digest"] = hashlib.sha1(b"".join(g.cpu().numpy().tobytes() for g in grads)).hexdigest()[:16]
+        for with_saved in (False, True):  # forward outputs of both instantiations
+            sigma.zero_(), rgb.zero_()
+            fwd(with_saved)
+            torch.cuda.synchronize()
+            res[f"{prec}_out_digest_{'train' if with_saved else 'infer'}"] = hashlib.sha1(
+                sigma.cpu().numpy().tobytes() + rgb.cpu().numpy().tobytes()).hexdigest()[:16]
         flop = 2.0 * 589_952 * N
         for k, evs in times.items():
             ms = sorted(a.elapsed_time(b) for a, b in evs)

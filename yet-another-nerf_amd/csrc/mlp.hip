@@ -25,34 +25,8 @@
 
 #include "common.hpp"
 
-// Development-only timing ablations (never set in the product build): 1 = no MFMA, 2 = no harmonic embedding,
-// 4 = no saved stores in the trunk epilogue, 8 = no VALU heads, 16 = no trunk LDS writes, 32 = no trunk barriers,
-// 64 = dX colour-head backward without its mask / weight math, 128 = dX without its point-major copies, 256 = bf16
-// GEMMs read only the first K-block of weights (L1-resident: the weight stream from L2 removed).
-#ifndef YANERF_F32_DB
-#define YANERF_F32_DB 0  // fp32 GEMM loop: double-buffered weight fragments (0: one set + copy, the earlier loop)
-#endif
-#ifndef YANERF_PRIO
-#define YANERF_PRIO 0  // fp32 GEMM loop: 1 = raise the wave priority over its MFMA block (A/B variant)
-#endif
-#ifndef YANERF_ABLATE
-#define YANERF_ABLATE 0
-#endif
-// bf16 forward wave tile: 4 waves x (64 features x 128 points) -- half the LDS operand reads per MFMA of the 8-wave
-// (32 x 128) tiling, twice the accumulators; measured training forward 1.47 -> 1.26 ms, inference 0.92 -> 0.77 ms.
-// The dX kernel uses the same 4-wave tiling (two workgroups per CU: one's GEMM covers the other's store drain) since
-// its loop-invariant fragment addresses stopped spilling (gemm_run's opaque lane id) and its colour head writes whole
-// LDS chunks: fine-pass dX 1.40 (8 waves) -> 1.26 ms. The ReLU-mask words the forward writes land in the dX kernel's
-// layout either way (mask_w).
-#ifndef YANERF_BF16_WAVES
-#define YANERF_BF16_WAVES 4
-#endif
-#ifndef YANERF_BF16_DXWAVES
-#define YANERF_BF16_DXWAVES 4
-#endif
-#ifndef YANERF_LOWREG
-#define YANERF_LOWREG 0
-#endif
+// The measured alternatives of rounds 1-3 (build macros selecting A/B variants and timing ablations) were removed in
+// round 4; every variant below is the measured default. DESIGN.md §9 lists them with the commits that measured them.
 
 namespace yanerf {
 
@@ -65,60 +39,30 @@ struct x3_t {};
 // per precision: point tile M, waves per workgroup, elements per 16-byte chunk (EPC) and per 64-byte K-block (KB),
 // weight-ring depth, occupancy target (waves per SIMD), operand planes, and the element types of the LDS tile,
 // of the saved activations / gradients in HBM and of the packed weights
+//
+// fp32: 64-point tiles, 4 waves, two workgroups per CU (WPE); 32-point tiles at 3-4 workgroups per CU, two tiles per
+// workgroup and 5-wave store-wave workgroups all measured slower.
+// bf16: 4 waves x (64 features x 128 points) for the forward and the dX kernel -- half the LDS operand reads per MFMA of
+// an 8-wave (32 x 128) tiling: training forward 1.47 -> 1.26 ms, dX 1.40 -> 1.26 ms (round 1). PM: saved activations /
+// backward gradients stored point-major in per-section arrays ([Npad][width], written from the LDS tile with 16-byte
+// stores, read by the dW kernel with transposed LDS reads) instead of feature-major rows.
 template <typename T> struct Cfg;
-#ifndef YANERF_BF16_PM
-#define YANERF_BF16_PM 1
-#endif
-#ifndef YANERF_PM_SPTS
-#define YANERF_PM_SPTS 64  // points per point-major dW stage (PM_SPTS below)
-#endif
-// PM: saved activations / backward gradients stored point-major in per-section arrays ([Npad][width], written from the
-// LDS tile with 16-byte stores, read by the dW kernel with transposed LDS reads) instead of feature-major rows
-#ifndef YANERF_F32_M
-#define YANERF_F32_M 64
-#endif
-#ifndef YANERF_F32_HALVES
-#define YANERF_F32_HALVES 1
-#endif
-#ifndef YANERF_F32_WPE
-#define YANERF_F32_WPE 2
-#endif
-// HALVES (forward kernel): 2 = one workgroup holds two independent point tiles (one per 4-wave half, each with its own
-// LDS image) and the second half runs one barrier segment behind the first, so on every SIMD one wave's GEMM runs
-// beside the other's epilogue (the two halves alternate GEMM / epilogue between the shared barriers); 1 = one tile.
-#ifndef YANERF_BF16_PP
-#define YANERF_BF16_PP 1
-#endif
-// with HALVES = 2: 1 = the second half runs one barrier segment behind the first (GEMM beside epilogue); 0 = both halves
-// in phase (the pair of waves on a SIMD read the same weight fragments at about the same time: one L2 -> CU stream
-// for 256 points)
-#ifndef YANERF_PP_SHIFT
-#define YANERF_PP_SHIFT 1
-#endif
 template <> struct Cfg<float> {
-  static constexpr int M = YANERF_F32_M, WAVES = 4, DXWAVES = 4, EPC = 4, KB = 16, APREF = 1, LOWREG = 0,
-                       WPE = YANERF_F32_WPE, PLANES = 1, HALVES = YANERF_F32_HALVES;
+  static constexpr int M = 64, WAVES = 4, DXWAVES = 4, EPC = 4, KB = 16, APREF = 1, WPE = 2, PLANES = 1;
   static constexpr bool PM = false;
   typedef float lds_t;
   typedef float st_t;
   typedef float w_t;
 };
 template <> struct Cfg<bf16_t> {
-  static constexpr int M = 128, WAVES = YANERF_BF16_WAVES, DXWAVES = YANERF_BF16_DXWAVES, EPC = 8, KB = 32,
-                       APREF = YANERF_BF16_WAVES == 4 ? 2 : 3, LOWREG = YANERF_LOWREG, WPE = LOWREG ? 4 : 2,
-                       HALVES = YANERF_BF16_PP;
-  static constexpr int PLANES = 1;
-  static constexpr bool PM = YANERF_BF16_PM;
+  static constexpr int M = 128, WAVES = 4, DXWAVES = 4, EPC = 8, KB = 32, APREF = 2, WPE = 2, PLANES = 1;
+  static constexpr bool PM = true;
   typedef bf16_t lds_t;
   typedef bf16_t st_t;
   typedef bf16_t w_t;
 };
-#ifndef YANERF_X3_APREF
-#define YANERF_X3_APREF 2
-#endif
 template <> struct Cfg<x3_t> {
-  static constexpr int M = 64, WAVES = 8, DXWAVES = 8, EPC = 8, KB = 32, APREF = YANERF_X3_APREF, LOWREG = 0, WPE = 2,
-                       PLANES = 3, HALVES = 1;
+  static constexpr int M = 64, WAVES = 8, DXWAVES = 8, EPC = 8, KB = 32, APREF = 2, WPE = 2, PLANES = 3;
   static constexpr bool PM = false;
   typedef bf16_t lds_t;
   typedef float st_t;
@@ -225,17 +169,11 @@ __host__ __device__ inline int64_t row_ld(int64_t Npad, size_t es) {
 // only (the dX kernel uses the ReLU mask words, never the activations), and the dW tile widens them back to bf16 (exact)
 // for the bf16 MFMA. Measured on a trained model (procedural scene, 3k steps): dW relative L2 error 0.6-0.9 % from the
 // fp8 rounding, against 0.03 % from bf16 storage and >10 % from the bf16 forward chain itself. Layout: byte offsets of
-// [Npad][width] sections. YANERF_BF16_A8=0 keeps every section in bf16 (A/B builds).
-#ifndef YANERF_BF16_A8
-#define YANERF_BF16_A8 1
-#endif
-constexpr int PM_HB = YANERF_BF16_A8 ? 1 : 2;  // bytes per saved H / C element
+// [Npad][width] sections (round-2 A/B: bf16 backward 2.85 -> 2.16 ms against bf16 sections).
+constexpr int PM_HB = 1;  // bytes per saved H / C element
 // Y (intermediate_linear's output, signed, the X operand of color_layer.0's weight gradient only) as fp8 e4m3 with a
-// power-of-two scale per 128-point tile, like the backward's gradient rows (YANERF_BF16_G8)
-#ifndef YANERF_BF16_Y8
-#define YANERF_BF16_Y8 1
-#endif
-constexpr int PM_YB = YANERF_BF16_Y8 ? 1 : 2;
+// power-of-two scale per 128-point tile, like the backward's gradient rows
+constexpr int PM_YB = 1;
 struct PmSave {
   int64_t pe, h0, y, dpe, c, ysc, total;
 };
@@ -263,17 +201,14 @@ static int64_t pm_sec_bytes(int L, int64_t Npad, int64_t r0, int* es, int64_t* s
   }
   if (r0 == SR.y) {
     *es = PM_YB;
-    if (scale_off && YANERF_BF16_Y8) *scale_off = PS.ysc;
+    if (scale_off) *scale_off = PS.ysc;
     return PS.y;
   }
   if (r0 == SR.dpe) return PS.dpe;
   *es = PM_HB;
   return PS.c;  // r0 == SR.c
 }
-#ifndef YANERF_BF16_G8
-#define YANERF_BF16_G8 1
-#endif
-constexpr int PM_GB = YANERF_BF16_G8 ? 1 : 2;  // bytes per dZ / dY / dZc element in the bf16 backward workspace
+constexpr int PM_GB = 1;  // bytes per dZ / dY / dZc element in the bf16 backward workspace (fp8 e4m3, scaled)
 // bf16 backward workspace (point-major): byte offsets of the gradient sections, the dU section (bf16: du_j at column j,
 // dsigma at PM_DSIG) and the per-(section, 128-point tile) fp8 scales (float; sections dZ_0..dZ_{L-1}, dY, dZc)
 struct PmGrad {
@@ -311,7 +246,7 @@ static int64_t pm_grad_sec(int L, int64_t Npad, int64_t r0, int* es, int64_t* sc
     *es = 2;
     return PG.du;
   }
-  if (YANERF_BF16_G8) *scale_off = PG.scale + 4LL * sec * (Npad / 128);
+  *scale_off = PG.scale + 4LL * sec * (Npad / 128);
   return off;
 }
 // backward workspace bytes before the dW slabs
@@ -327,12 +262,9 @@ static int64_t saved_t_bytes(int L, int64_t Npad, size_t es, bool pm) {
 static int64_t tile_m(int prec) {
   return prec == YANERF_PREC_F32 ? Cfg<float>::M : prec == YANERF_PREC_BF16 ? Cfg<bf16_t>::M : Cfg<x3_t>::M;
 }
-static int64_t fwd_halves(int prec) {
-  return prec == YANERF_PREC_F32 ? Cfg<float>::HALVES : prec == YANERF_PREC_BF16 ? Cfg<bf16_t>::HALVES : Cfg<x3_t>::HALVES;
-}
-// Npad: a multiple of the forward workgroup's points (HALVES tiles of M), so every workgroup holds whole tiles
+// Npad: a multiple of the point tile, so every workgroup holds a whole tile
 static int64_t npad_of(int prec, int64_t n) {
-  const int64_t M = tile_m(prec) * fwd_halves(prec);
+  const int64_t M = tile_m(prec);
   return (n + M - 1) / M * M;
 }
 // element size of the saved activations / gradient rows (fp32 for both fp32 modes)
@@ -587,13 +519,6 @@ template <> __device__ __forceinline__ f4 mma_blk<x3_t>(f4 a, f4 b, f4 c) { retu
 // the b side)
 template <typename T, int NI, int NJ, bool SWAP = false>
 __device__ __forceinline__ void mma_grid(const f4 (&a)[NI], const f4 (&b)[NJ], f4 (&acc)[NI][NJ]) {
-  if constexpr (YANERF_ABLATE & 1) {
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] += a[i] * b[j].x;
-    return;
-  }
   if constexpr (sizeof(T) == 4) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -632,7 +557,7 @@ __device__ __forceinline__ void ring_fill(ARing<T, NT>& R, const typename Cfg<T>
     if constexpr (OPQ) asm volatile("" : "+v"(lane));
 #pragma unroll
     for (int r = 0; r < D; ++r) {
-      const int k = (YANERF_ABLATE & 256) ? 0 : (r < nkb ? r : nkb - 1);
+      const int k = r < nkb ? r : nkb - 1;
 #pragma unroll
       for (int pl = 0; pl < NP; ++pl)
 #pragma unroll
@@ -646,68 +571,27 @@ __device__ __forceinline__ void ring_fill(ARing<T, NT>& R, const typename Cfg<T>
 // Accumulator layout: acc[nt][mt] lane (g, li) holds features nrow0 + 16nt + 4g .. +3 of point 16mt + li. The
 // accumulators start from the bias when one is given (the reference's addmm also accumulates onto the bias).
 // fp32 forward: the saved rows of the GEMM's input (post-ReLU H of the previous layer, as the LDS tile holds it) are
-// written from the B fragments during the GEMM instead of from the accumulators in the previous epilogue
-// (YANERF_F32_GSAVE). Wave w stores K-blocks kb = w, w + 4, ... (all of the tile's points), after that K-block's MFMAs:
-// each weight wait then covers the stores of one earlier K-block rather than the whole epilogue's burst.
-#ifndef YANERF_F32_GSAVE
-#define YANERF_F32_GSAVE 1
-#endif
-#ifndef YANERF_F32_GSAVE_DX
-#define YANERF_F32_GSAVE_DX 1
-#endif
+// written from the B fragments during the GEMM instead of from the accumulators in the previous epilogue. Wave w stores
+// K-blocks kb = w, w + 4, ... (all of the tile's points), after that K-block's MFMAs: each weight wait then covers the
+// stores of one earlier K-block rather than the whole epilogue's burst (training forward 7.78 -> 7.61 ms). The fp32 dX
+// does the same for dY and dZ_l, with a K-block's stores BEFORE its MFMAs (6.88 ms, against 7.29 ms after them).
 // RSV (gemm_run / gemm_lds template argument): 0 no row stores, 1 a K-block's stores after its MFMAs (the forward),
-// 2 before them (the dX kernel). Measured both ways in both kernels: forward 7.58 (after) vs 7.74 ms (before); dX
-// 7.29 (after) vs 6.88 ms (before), against 7.19 ms with epilogue stores.
+// 2 before them (the dX kernel).
+constexpr int RSV_FWD = 1, RSV_DX = 2;
 // fp32 saved / gradient rows with non-temporal stores (the rows are read back by the dW kernel milliseconds and
-// gigabytes later, never from L2; the weight fragments the GEMMs stream share that L2). Measured
-// (profiles/r3_ab_fp32_save_nt.jsonl, r3_ab_x3_save_nt.jsonl): fp32 training forward 7.59-7.61 -> 7.53 ms, dX flat,
-// bitwise-equal gradients; x3 slower (dX 4.43 -> 4.56-4.60 ms), so x3 keeps plain stores.
-#ifndef YANERF_F32_SAVE_NT
-#define YANERF_F32_SAVE_NT 1
-#endif
-template <bool NT = (YANERF_F32_SAVE_NT != 0)>
+// gigabytes later, never from L2; the weight fragments the GEMMs stream share that L2): training forward 7.59 -> 7.53
+// ms, bitwise equal. x3 keeps plain stores (its dX measured 4.43 -> 4.56 ms with them).
+template <bool NT = true>
 __device__ __forceinline__ void st_row_f32(const char* p, float v) {
   if constexpr (NT) __builtin_nontemporal_store(v, (float*)p);
   else *(float*)p = v;
 }
-// x3 forward: the saved H rows from the next GEMM's three-plane B fragments, as the fp32 forward does. Bitwise-equal
-// gradients, not faster (training forward 5.01-5.02 vs 4.92-5.01 ms, profiles/r3_ab_x3_fwd_gsave.jsonl): kept off.
-#ifndef YANERF_X3_GSAVE
-#define YANERF_X3_GSAVE 0
-#endif
-// fp32 GEMM loop: the copy of the prefetched weight fragments into the current set pinned after the K-block's MFMAs
-// (1: every GEMM, 2: the GEMMs without in-GEMM row stores). Left free, the compiler interleaves the 16 copies with the
-// MFMAs and so waits for the next block's loads a quarter of the way into the current one. Measured
-// (profiles/r3_ab_fp32_latecopy_all.jsonl, r3_ab_fp32_latecopy_storefree.jsonl; bitwise equal): inference forward
-// 7.04-7.09 -> 6.93-6.98 ms; the training forward is unchanged (its row stores already sit between the MFMAs and the
-// copies) and the dX slower with it (6.90 -> 7.19 ms), so 2.
-// training / inference forward as separate instantiations with the saves' presence known at compile time (STAT; else
-// the kernel tests the saved pointer at run time). With the run-time test the compiler merges the saving and
-// non-saving paths, and at the next GEMM's first weight use waits with vmcnt(0) -- for the previous epilogue's saved-row
-// and mask stores too -- instead of counting past them. Measured (profiles/r3_ab_static_save_instantiation.jsonl,
-// bitwise equal): x3 training forward 4.97-5.00 -> 4.86-4.88 ms, fp32 7.57 -> 7.51-7.54 ms.
-#ifndef YANERF_X3_STAT
-#define YANERF_X3_STAT 1
-#endif
-#ifndef YANERF_F32_STAT
-#define YANERF_F32_STAT 1
-#endif
-#ifndef YANERF_F32_LATECOPY
-#define YANERF_F32_LATECOPY 2
-#endif
-#ifndef YANERF_F32_GSAVE_POS_FWD
-#define YANERF_F32_GSAVE_POS_FWD 1
-#endif
-#ifndef YANERF_F32_GSAVE_POS_DX
-#define YANERF_F32_GSAVE_POS_DX 2
-#endif
 struct RowSave {
   float* base;    // saved row of the GEMM's feature 0 at the tile's first point
   uint32_t voff;  // this lane's byte offset in a 16x16 row tile (4g rows + li points)
   int ldb;        // row stride, bytes
   int nkb;        // K-blocks to store (the H columns; a skip layer's PE columns are saved elsewhere)
   int wave, waves;
-  int64_t blk = 0;  // (YANERF_ABLATE & 2048, timing only) byte offset of the tile's contiguous block from base
 };
 
 template <typename T, int NT, int MT, int RSV = 0>
@@ -766,31 +650,6 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) ar[pl][nt] = *(const f4*)(wp[nt] + pl * wplane + ka * FRAG);
       }
-      if constexpr (RSV != 0) {
-        // x3 in-GEMM saves (YANERF_X3_GSAVE): this K-block's fp32 rows rebuilt from its three bf16 planes, t0 + (t1 +
-        // t2) == v exactly (lds_put / pk_lds split v so that every residual is exact), stored after the weight refill
-        __builtin_amdgcn_sched_barrier(0);
-        if (kb < rs.nkb && kb % rs.waves == rs.wave) {
-          const char* rb = (const char*)rs.base + (int64_t)(32 * kb) * rs.ldb;
-          uint32_t vo = (uint32_t)(8 * g * rs.ldb + 4 * li);
-          asm volatile("" : "+v"(vo));
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const uint32_t o = vo + 16 * mt * 4;
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-              const uint32_t w0 = __float_as_uint(b[0][mt][d]), w1 = __float_as_uint(b[1][mt][d]),
-                             w2 = __float_as_uint(b[2][mt][d]);
-              const float lo = __uint_as_float(w0 << 16) + (__uint_as_float(w1 << 16) + __uint_as_float(w2 << 16));
-              const float hi = __uint_as_float(w0 & 0xffff0000u) +
-                               (__uint_as_float(w1 & 0xffff0000u) + __uint_as_float(w2 & 0xffff0000u));
-              st_row_f32<false>(rb + o + (uint32_t)(2 * d) * (uint32_t)rs.ldb, lo);
-              st_row_f32<false>(rb + o + (uint32_t)(2 * d + 1) * (uint32_t)rs.ldb, hi);
-            }
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
@@ -804,39 +663,6 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
 #pragma unroll
     for (int r = 0; r < D - 1; ++r)
       if (kb + r < nkb) step(kb + r, a[r], false);
-    return;
-  }
-  if constexpr (sizeof(T) == 2 && Cfg<T>::LOWREG) {
-    // two workgroups per CU (<= 128 VGPRs): no LDS double buffer, a 2-deep weight ring; the other workgroup's
-    // waves cover the LDS / L2 latency
-    constexpr int D = 2;
-    f4 a[D][NT];
-#pragma unroll
-    for (int r = 0; r < D; ++r) {
-      const int k = r < nkb ? r : nkb - 1;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) a[r][nt] = *(const f4*)(wp[nt] + k * FRAG);
-    }
-    auto step = [&](int kb, f4(&ar)[NT], bool refill) {
-      f4 bq[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) bq[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + kb * 4 + g);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[nt][mt] = mma_blk<T>(ar[nt], bq[mt], acc[nt][mt]);
-      if (refill) {
-        const int ka = kb + D < nkb ? kb + D : nkb - 1;
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) ar[nt] = *(const f4*)(wp[nt] + ka * FRAG);
-      }
-    };
-    int kb = 0;
-    for (; kb + D <= nkb; kb += D) {
-#pragma unroll
-      for (int r = 0; r < D; ++r) step(kb + r, a[r], true);
-    }
-    if (kb < nkb) step(kb, a[0], false);
     return;
   }
   if constexpr (sizeof(T) == 2 && MT == 8 && NT >= 4) {
@@ -867,7 +693,7 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
         for (int mt = 0; mt < MH; ++mt) acc[nt][mt + MH] = mma_blk<T>(ar[nt], b1[mt], acc[nt][mt + MH]);
       __builtin_amdgcn_sched_barrier(0);
       if (refill) {
-        const int ka = (YANERF_ABLATE & 256) ? 0 : (kb + D < nkb ? kb + D : nkb - 1);
+        const int ka = kb + D < nkb ? kb + D : nkb - 1;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) ar[nt] = *(const f4*)(wp[nt] + ka * FRAG);
       }
@@ -916,36 +742,29 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
       if (kb + r < nkb) step(kb + r, a[r][0], false);
     return;
   }
-  if constexpr (YANERF_F32_DB) {
-    // fp32: the weight fragments are double-buffered in two static register sets (loop unrolled by two). Block
-    // kb+1's loads are issued before block kb's 64 MFMAs and pinned there by scheduling barriers, so each L2 round
-    // trip hides behind a whole K-block. (With one set and a copy, the compiler sank the loads to the end of the
-    // iteration and waited for them a few MFMAs later: an exposed L2 latency per K-block.)
-    f4 a0[NT], a1[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) a0[nt] = *(const f4*)(wp[nt]);
-    auto half = [&](int kb, const f4(&acur)[NT], f4(&anext)[NT]) {
-      const int kn = kb + 1 < nkb ? kb + 1 : kb;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) anext[nt] = *(const f4*)(wp[nt] + kn * FRAG);
-      if constexpr (YANERF_F32_DB == 1) __builtin_amdgcn_sched_barrier(0);
-      f4 b[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) b[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + kb * 4 + g);
-      mma_grid<T, NT, MT>(acur, b, acc);
-      if constexpr (YANERF_F32_DB == 1) __builtin_amdgcn_sched_barrier(0);
-    };
-    int kb = 0;
-    for (; kb + 2 <= nkb; kb += 2) {
-      half(kb, a0, a1);
-      half(kb + 1, a1, a0);
-    }
-    if (kb < nkb) half(kb, a0, a1);
-    return;
-  }
+  // fp32: one weight-fragment set plus the next block's prefetch (two static register sets and a 2-block lookahead
+  // measured slower)
   f4 a[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) a[nt] = *(const f4*)(wp[nt]);
+  // this K-block's in-GEMM row stores (wave w stores K-blocks w, w + waves, ...): a uniform 64-bit base of the K-block's
+  // 16 rows and 32-bit lane offsets (an opaque copy, so the compiler does not hoist 64-bit addresses for every K-block
+  // out of the caller's layer loop)
+  auto row_stores = [&](int kb, const f4(&b)[MT]) {
+    if (kb < rs.nkb && kb % rs.waves == rs.wave) {
+      const char* rb = (const char*)rs.base + (int64_t)(16 * kb) * rs.ldb;
+      uint32_t vo = rs.voff;
+      asm volatile("" : "+v"(vo));
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const uint32_t o = vo + 16 * mt * 4;
+        st_row_f32(rb + o, b[mt].x);
+        st_row_f32(rb + o + (uint32_t)rs.ldb, b[mt].y);
+        st_row_f32(rb + o + 2u * (uint32_t)rs.ldb, b[mt].z);
+        st_row_f32(rb + o + 3u * (uint32_t)rs.ldb, b[mt].w);
+      }
+    }
+  };
   for (int kb = 0; kb < nkb; ++kb) {
     f4 an[NT];
     const int kn = (kb + 1 < nkb) ? kb + 1 : kb;
@@ -954,72 +773,22 @@ __device__ __forceinline__ void gemm_run(const typename Cfg<T>::w_t* __restrict_
     f4 b[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) b[mt] = lds_chunk<T>(act, 16 * mt + li, kc0 + kb * 4 + g);
-    if constexpr (RSV == 2) {
+    if constexpr (RSV == RSV_DX) {
       __builtin_amdgcn_sched_barrier(0);
-      if ((YANERF_ABLATE & 2048) && kb < rs.nkb && kb % rs.waves == rs.wave) {
-        // timing ablation: the same stores, each wave-instruction writing 256 contiguous bytes of a per-tile block
-        const char* bb = (const char*)rs.base + rs.blk + (int64_t)kb * 4096;
-        uint32_t vo = (uint32_t)((g * 16 + li) * 4);
-        asm volatile("" : "+v"(vo));
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          st_row_f32(bb + vo + (0 * 4 + mt) * 256, b[mt].x);
-          st_row_f32(bb + vo + (1 * 4 + mt) * 256, b[mt].y);
-          st_row_f32(bb + vo + (2 * 4 + mt) * 256, b[mt].z);
-          st_row_f32(bb + vo + (3 * 4 + mt) * 256, b[mt].w);
-        }
-      } else if (kb < rs.nkb && kb % rs.waves == rs.wave) {
-        // uniform 64-bit base of the K-block's 16 rows, 32-bit lane offsets (an opaque copy, so the compiler does not
-        // hoist 64-bit addresses for every K-block out of the caller's layer loop)
-        const char* rb = (const char*)rs.base + (int64_t)(16 * kb) * rs.ldb;
-        uint32_t vo = rs.voff;
-        asm volatile("" : "+v"(vo));
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const uint32_t o = vo + 16 * mt * 4;
-          st_row_f32(rb + o, b[mt].x);
-          st_row_f32(rb + o + (uint32_t)rs.ldb, b[mt].y);
-          st_row_f32(rb + o + 2u * (uint32_t)rs.ldb, b[mt].z);
-          st_row_f32(rb + o + 3u * (uint32_t)rs.ldb, b[mt].w);
-        }
-      }
+      row_stores(kb, b);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (YANERF_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     mma_grid<T, NT, MT>(a, b, acc);
-    if constexpr (YANERF_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-    if constexpr (RSV == 1) {
+    if constexpr (RSV == RSV_FWD) {
       __builtin_amdgcn_sched_barrier(0);
-      if ((YANERF_ABLATE & 2048) && kb < rs.nkb && kb % rs.waves == rs.wave) {
-        // timing ablation: the same stores, each wave-instruction writing 256 contiguous bytes of a per-tile block
-        const char* bb = (const char*)rs.base + rs.blk + (int64_t)kb * 4096;
-        uint32_t vo = (uint32_t)((g * 16 + li) * 4);
-        asm volatile("" : "+v"(vo));
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          st_row_f32(bb + vo + (0 * 4 + mt) * 256, b[mt].x);
-          st_row_f32(bb + vo + (1 * 4 + mt) * 256, b[mt].y);
-          st_row_f32(bb + vo + (2 * 4 + mt) * 256, b[mt].z);
-          st_row_f32(bb + vo + (3 * 4 + mt) * 256, b[mt].w);
-        }
-      } else if (kb < rs.nkb && kb % rs.waves == rs.wave) {
-        // uniform 64-bit base of the K-block's 16 rows, 32-bit lane offsets (an opaque copy, so the compiler does not
-        // hoist 64-bit addresses for every K-block out of the caller's layer loop)
-        const char* rb = (const char*)rs.base + (int64_t)(16 * kb) * rs.ldb;
-        uint32_t vo = rs.voff;
-        asm volatile("" : "+v"(vo));
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const uint32_t o = vo + 16 * mt * 4;
-          st_row_f32(rb + o, b[mt].x);
-          st_row_f32(rb + o + (uint32_t)rs.ldb, b[mt].y);
-          st_row_f32(rb + o + 2u * (uint32_t)rs.ldb, b[mt].z);
-          st_row_f32(rb + o + 3u * (uint32_t)rs.ldb, b[mt].w);
-        }
-      }
+      row_stores(kb, b);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (YANERF_F32_LATECOPY == 1 || (YANERF_F32_LATECOPY == 2 && RSV == 0)) __builtin_amdgcn_sched_barrier(0);
+    // GEMMs without row stores: the copy of the prefetched fragments pinned after the K-block's MFMAs (left free, the
+    // compiler interleaves the copies with the MFMAs and waits for the next block's loads a quarter of the way into
+    // this one): inference forward 7.04 -> 6.93 ms; with row stores (already between the MFMAs and the copies) the dX
+    // measured slower pinned (6.90 -> 7.19 ms)
+    if constexpr (RSV == 0) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) a[nt] = an[nt];
   }
@@ -1117,15 +886,10 @@ template <> __device__ __forceinline__ void pk_lds<x3_t>(bf16_t* act, int m, int
   pk_lds<bf16_t>(act + PL, m, n, h1);
   pk_lds<bf16_t>(act + 2 * PL, m, n, h2);
 }
-// Store a packed tile into 4 feature-major rows given the tile's uniform base (layer, row tile, point tile: SGPRs),
-// this lane's byte offset `voff` (4g rows + li points, one VGPR for every tile), the row stride `ldb` and the byte
-// offset `so` of the 16-point group.
-//  bf16: raw buffer stores (voffset = lane, soffset = row / point-group offset): no per-store 64-bit address VALU,
-//        which the 2-byte stores (4 per tile) otherwise pay (measured: bf16 inference forward 0.99 -> 0.90 ms with the
-//        SAVE template);
-//  fp32 / x3: plain global stores (buffer stores measured slower there: fp32 training forward 7.7 -> 8.4 ms).
-// All plain (temporal) stores: the scattered 2-/4-byte row segments rely on write-combining in L2 (measured:
-// non-temporal stores made the bf16 forward 2.6x slower).
+// Store a packed tile into 4 feature-major rows (fp32 / x3; bf16 stores point-major sections, copy_tile_pm) given the
+// tile's uniform base (layer, row tile, point tile: SGPRs), this lane's byte offset `voff` (4g rows + li points, one VGPR
+// for every tile), the row stride `ldb` and the byte offset `so` of the 16-point group. Plain global stores (buffer
+// stores measured slower here: fp32 training forward 7.7 -> 8.4 ms); fp32 non-temporal, x3 temporal (st_row_f32).
 template <typename T>
 __device__ __forceinline__ void pk_store_rows_b(typename Cfg<T>::st_t* base, uint32_t voff, int ldb, int so, Pk<T> p);
 template <>
@@ -1143,14 +907,6 @@ __device__ __forceinline__ void pk_store_rows_b<x3_t>(float* base, uint32_t voff
   st_row_f32<false>(b + ldb, p.v.y);
   st_row_f32<false>(b + 2 * (int64_t)ldb, p.v.z);
   st_row_f32<false>(b + 3 * (int64_t)ldb, p.v.w);
-}
-template <>
-__device__ __forceinline__ void pk_store_rows_b<bf16_t>(bf16_t* base, uint32_t voff, int ldb, int so, Pk<bf16_t> p) {
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b16((unsigned short)p.w0, rs, voff, so, 0);
-  __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(p.w0 >> 16), rs, voff, so + ldb, 0);
-  __builtin_amdgcn_raw_buffer_store_b16((unsigned short)p.w1, rs, voff, so + 2 * ldb, 0);
-  __builtin_amdgcn_raw_buffer_store_b16((unsigned short)(p.w1 >> 16), rs, voff, so + 3 * ldb, 0);
 }
 
 // Per-lane trunk ReLU mask words of one layer: 4 bits for each of the lane's NT*MT accumulator tiles, tile t in
@@ -1278,10 +1034,9 @@ __device__ __forceinline__ void store_mask_tile(uint64_t* masks, int64_t Npad, i
   if (lane < 4) masks[mask_index(Npad, slot, pt16, ft) + lane] = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
 }
 
-// cache-policy bits of the point-major saves' buffer stores (gfx950: 1 sc0, 2 nt, 16 sc1)
-#ifndef YANERF_STORE_AUX
-#define YANERF_STORE_AUX 2  // nt: measured bf16 backward -2.5 %, forward unchanged (sc0 / sc1: no gain)
-#endif
+// cache-policy bits of the point-major saves' buffer stores (gfx950: 1 sc0, 2 nt, 16 sc1): nt measured bf16 backward
+// -2.5 %, forward unchanged (sc0 / sc1: no gain)
+constexpr int PM_STORE_AUX = 2;
 // Point-major (Cfg::PM) save: columns [col0, col0 + W) of the LDS tile's M points -> the [Npad][W] section at
 // dst = section + p0 * W. A lane moves one 16-byte chunk: a 16-lane group reads 256 contiguous bytes of one LDS row
 // (the row swizzle permutes chunks within aligned groups of 8) and a wave-instruction writes 1 KiB contiguously.
@@ -1314,11 +1069,11 @@ __device__ __forceinline__ void copy_tile_pm(const typename Cfg<T>::lds_t* act, 
 #pragma unroll
     for (int i = 0; i < GRP; ++i)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint32_t __attribute__((ext_vector_type(4))), v[i]), rs,
-                                             goff + (uint32_t)((i0 + i) * NTHR * 16), 0, YANERF_STORE_AUX);
+                                             goff + (uint32_t)((i0 + i) * NTHR * 16), 0, PM_STORE_AUX);
   }
 }
 
-// The fp8 save of a point-major section (YANERF_BF16_A8): like copy_tile_pm, but a lane reads two 16-byte LDS chunks
+// The fp8 save of a point-major section: like copy_tile_pm, but a lane reads two 16-byte LDS chunks
 // (16 bf16 features of one point), converts them to 16 fp8 e4m3 (clamped to 448: the tile holds post-ReLU values, so
 // an integer min on the bf16 bits is the clamp) and writes one 16-byte chunk; a wave-instruction writes 1 KiB
 // contiguously.
@@ -1369,19 +1124,18 @@ __device__ __forceinline__ void copy_tile_pm_fp8(const typename Cfg<T>::lds_t* a
                          fp8x4_from_bf16<CLAMP>(__float_as_uint(hi[i].z), __float_as_uint(hi[i].w), scale)};
       // offset in the VGPR offset, soffset = 0 (the wide-store hazard note at copy_tile_pm); the nop keeps the next
       // group's LDS reads (which reuse these VGPRs) one instruction away from the store
-      __builtin_amdgcn_raw_buffer_store_b128(out, rs, goff + (uint32_t)((i0 + i) * NTHR * 16), 0, YANERF_STORE_AUX);
+      __builtin_amdgcn_raw_buffer_store_b128(out, rs, goff + (uint32_t)((i0 + i) * NTHR * 16), 0, PM_STORE_AUX);
       asm volatile("s_nop 0" ::: "memory");
     }
   }
 }
-// save of a post-ReLU section: fp8 (YANERF_BF16_A8) or bf16
+// save of a post-ReLU section as fp8
 template <typename T, int NTHR, int W>
 __device__ __forceinline__ void save_relu_pm(const typename Cfg<T>::lds_t* act, int col0, char* dst, int tid) {
-  if constexpr (YANERF_BF16_A8) copy_tile_pm_fp8<T, NTHR, W>(act, col0, (uint8_t*)dst, tid);
-  else copy_tile_pm<T, NTHR, W>(act, col0, (typename Cfg<T>::st_t*)dst, tid);
+  copy_tile_pm_fp8<T, NTHR, W>(act, col0, (uint8_t*)dst, tid);
 }
 
-// fp8 gradient rows (YANERF_BF16_G8): the dX kernel's pre-activation gradients dZ_l, dY and dZc are the dW kernel's A
+// fp8 gradient rows: the dX kernel's pre-activation gradients dZ_l, dY and dZc are the dW kernel's A
 // operands only. Each leaves a tile as fp8 e4m3 of value / s with one power-of-two s per (section, 128-point tile),
 // chosen so the tile's largest |value| lands in [128, 256) (below e4m3's 448 after the bf16 rounding of the LDS copy);
 // s goes to a small scale array beside the rows and the dW tile widens the fragments with it (exact).
@@ -1424,19 +1178,15 @@ __device__ __forceinline__ float g8_scale(float amax) {
   return e <= 7u ? 1.0f : __uint_as_float((e - 7u) << 23);
 }
 // the gradient tile's save: `red` holds each wave's |max| of the section (written before the last barrier)
-template <typename T, int NTHR, int W, bool F8 = YANERF_BF16_G8>
+template <typename T, int NTHR, int W>
 __device__ __forceinline__ void save_grad_pm(const typename Cfg<T>::lds_t* act, char* dst, float* scale_out,
                                              const float* red, int waves, int tid) {
-  if constexpr (F8) {
-    float amax = red[0];
-    for (int w = 1; w < waves; ++w) amax = fmaxf(amax, red[w]);
-    const float sc = g8_scale(amax);
-    if (tid == 0) *scale_out = sc;
-    // two chunks in flight: the dX trunk step copies while the next layer's weight ring is live
-    copy_tile_pm_fp8<T, NTHR, W, false, 2>(act, 0, (uint8_t*)dst, tid, sc);
-  } else {
-    copy_tile_pm<T, NTHR, W>(act, 0, (typename Cfg<T>::st_t*)dst, tid);
-  }
+  float amax = red[0];
+  for (int w = 1; w < waves; ++w) amax = fmaxf(amax, red[w]);
+  const float sc = g8_scale(amax);
+  if (tid == 0) *scale_out = sc;
+  // two chunks in flight: the dX trunk step copies while the next layer's weight ring is live
+  copy_tile_pm_fp8<T, NTHR, W, false, 2>(act, 0, (uint8_t*)dst, tid, sc);
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global stores (the
@@ -1445,9 +1195,12 @@ __device__ __forceinline__ void save_grad_pm(const typename Cfg<T>::lds_t* act, 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ============================================================================================ forward
-// SAVE: training forward (saved activation rows + ReLU masks for the backward); else inference, outputs only.
+// SAVE: training forward (saved activation rows + ReLU masks for the backward); else inference, outputs only. The two
+// are separate instantiations, so the saves' presence is known at compile time: with a run-time saved-pointer test the
+// compiler waited vmcnt(0) at the next GEMM's first weight use, i.e. for the epilogue's stores too (x3 training forward
+// 4.97 -> 4.86 ms, fp32 7.57 -> 7.52 ms, bitwise equal).
 template <typename T, bool SAVE>
-__global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
+__global__ void __launch_bounds__(Cfg<T>::WAVES * 64)
     __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_fwd_kernel(
     MlpLayout lay, const typename Cfg<T>::w_t* __restrict__ Wt, const float* __restrict__ Wf,
     const float* __restrict__ origins, const float* __restrict__ dirs, const float* __restrict__ lengths, int64_t R,
@@ -1458,31 +1211,18 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB, TPP = WAVES * 64 / M;  // threads per point
   constexpr int MW = mask_w<T>();  // u64 ReLU-mask words per lane per layer
   typedef typename Cfg<T>::lds_t LT;
-  constexpr int HALVES = Cfg<T>::HALVES;
-  __shared__ __attribute__((aligned(16))) LT act_all[HALVES * Cfg<T>::PLANES * M * ROW];
-  // half h of the workgroup owns point tile `tile` with its own LDS image; everything below is per half
-  const int half = HALVES > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x / (WAVES * 64)) : 0;
-  LT* const act = act_all + half * Cfg<T>::PLANES * M * ROW;
-  const int tid = HALVES > 1 ? (int)threadIdx.x & (WAVES * 64 - 1) : (int)threadIdx.x, lane = tid & 63;
+  __shared__ __attribute__((aligned(16))) LT act[Cfg<T>::PLANES * M * ROW];
+  const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int64_t N = R * P;
-  const int64_t tile = HALVES > 1 ? (int64_t)blockIdx.x * HALVES + half : (int64_t)blockIdx.x;
-  const int64_t ntiles = HALVES > 1 ? (int64_t)gridDim.x * HALVES : (int64_t)gridDim.x;
+  const int64_t tile = (int64_t)blockIdx.x, ntiles = (int64_t)gridDim.x;
   const int64_t p0 = tile * M;
-  // ping-pong: the second half enters one barrier segment late (and the first half leaves with one extra barrier), so
-  // between two workgroup barriers one half runs a layer's GEMM while the other runs its epilogue
-  if (HALVES > 1 && YANERF_PP_SHIFT && half == 1) lds_barrier();
   typedef typename Cfg<T>::st_t ST;
   const int64_t ld = row_ld(Npad, sizeof(ST)), ldb = ld * (int64_t)sizeof(ST);
   const uint32_t soff = (uint32_t)(4 * g * ldb + li * (int64_t)sizeof(ST));  // this lane's offset in a 16x16 row tile
   if constexpr (!SAVE) saved = nullptr;
-  // bf16 has separate training / inference instantiations (branch-free epilogues); fp32 / x3 keep one kernel that
-  // tests the saved pointer at run time (with a branch-free epilogue the compiler interleaves it into the GEMM loop
-  // and the fp32 MFMA schedule measured slower: training forward 7.7 -> 8.3 ms)
-  constexpr bool STAT = (sizeof(T) == 2 && !is_x3<T>) || (is_x3<T> && YANERF_X3_STAT) ||
-                        (std::is_same<T, float>::value && YANERF_F32_STAT);
-  const bool sv = STAT ? SAVE : saved != nullptr;
+  constexpr bool sv = SAVE;
   const int64_t wpl = lay.t_plane;
   const SavedRows SR = saved_rows(lay.L);
   const PmSave PS = pm_save(lay.L, Npad);  // byte offsets of the point-major sections (bf16)
@@ -1502,9 +1242,8 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
   for (int i = 0; i < 3; ++i) x3[i] = o3[i] + t * d3[i];  // models/utils.py:244
   constexpr bool PM = Cfg<T>::PM;
   constexpr int NTHR = WAVES * 64;
-  if (!(YANERF_ABLATE & 2))
-    harmonic_to_lds<T>(act, mt_, PE_COL, KPE, x3, lay.fx, lay.ax, q,
-                       (saved && !PM) ? saved + SR.pe * ld + p : nullptr, ld);
+  harmonic_to_lds<T>(act, mt_, PE_COL, KPE, x3, lay.fx, lay.ax, q, (saved && !PM) ? saved + SR.pe * ld + p : nullptr,
+                     ld);
   lds_barrier();
 
   f4 acc[NT][MT];
@@ -1517,35 +1256,32 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
   // the store's write acknowledgement too. The GEMM of layer l + 1 still reads H_l from the LDS tile, so H_l (and the
   // mask words of layer l) leave during iteration l + 1, between its GEMM and its epilogue barrier.
   uint64_t pbits[MW] = {};
-  // fp32: H_l's saved rows leave from the B fragments of the GEMM that reads H_l (YANERF_F32_GSAVE); x3 likewise,
-  // rebuilt from its three planes (YANERF_X3_GSAVE)
-  constexpr bool GS = ((std::is_same<T, float>::value && YANERF_F32_GSAVE) || (is_x3<T> && YANERF_X3_GSAVE)) && SAVE;
+  // fp32: H_l's saved rows leave from the B fragments of the GEMM that reads H_l (gemm_run RSV_FWD)
+  constexpr bool GS = std::is_same<T, float>::value && SAVE;
   auto hsave = [&](int hl) {
     return RowSave{(sv && hl >= 0) ? (float*)(void*)(saved + (SR.h0 + 256LL * hl) * ld + p0) : nullptr, soff,
-                   (int)ldb, (sv && hl >= 0) ? 256 / KB : 0, wave, WAVES, p0 * 255 * (int64_t)sizeof(ST)};
+                   (int)ldb, (sv && hl >= 0) ? 256 / KB : 0, wave, WAVES};
   };
   for (int l = 0; l < lay.L; ++l) {
     const bool sk = (lay.skip >> l) & 1u;
     const int kc0 = (l == 0) ? PE_COL / EPC : 0;
     const int nkb = (l == 0) ? KPE / KB : (sk ? 320 / KB : 256 / KB);
-    gemm_lds<T, NT, MT, GS ? YANERF_F32_GSAVE_POS_FWD : 0>(Wt + lay.w_off[l], wpl, lay.kpad[l], nrow0, act, kc0, nkb, acc, lane, Wf + lay.b_off[l],
-                            &ring, hsave(l - 1));
+    gemm_lds<T, NT, MT, GS ? RSV_FWD : 0>(Wt + lay.w_off[l], wpl, lay.kpad[l], nrow0, act, kc0, nkb, acc, lane,
+                                          Wf + lay.b_off[l], &ring, hsave(l - 1));
     if (l + 1 < lay.L)
       ring_fill<T, NT>(ring, Wt + lay.w_off[l + 1], wpl, lay.kpad[l + 1], nrow0, lay.kpad[l + 1] / KB, lane);
     else ring_fill<T, NT>(ring, Wt + lay.wint_off, wpl, 256, nrow0, 256 / KB, lane);
-    if constexpr (PM) {
-      if (sv && !(YANERF_ABLATE & 4)) {
-        if (l == 0) {
-          copy_tile_pm<T, NTHR, KPE>(act, PE_COL, (ST*)((char*)saved + PS.pe) + p0 * KPE, tid);
-        } else {
-          save_relu_pm<T, NTHR, 256>(act, 0, (char*)saved + PS.h0 + ((l - 1) * Npad + p0) * 256LL * PM_HB, tid);
+    if constexpr (PM && sv) {
+      if (l == 0) {
+        copy_tile_pm<T, NTHR, KPE>(act, PE_COL, (ST*)((char*)saved + PS.pe) + p0 * KPE, tid);
+      } else {
+        save_relu_pm<T, NTHR, 256>(act, 0, (char*)saved + PS.h0 + ((l - 1) * Npad + p0) * 256LL * PM_HB, tid);
 #pragma unroll
-          for (int w = 0; w < MW; ++w)
-            masks[((((int64_t)(l - 1) * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
-        }
+        for (int w = 0; w < MW; ++w)
+          masks[((((int64_t)(l - 1) * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
       }
     }
-    if (!(YANERF_ABLATE & 32)) lds_barrier();
+    lds_barrier();
     uint64_t bits[MW] = {};
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -1554,12 +1290,11 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
       for (int mt = 0; mt < MT; ++mt) {
         const Pk<T> h = pk_relu<T>(pk_make<T>(acc[nt][mt]));
         const int m = 16 * mt + li;
-        if (!(YANERF_ABLATE & 16)) pk_lds<T>(act, m, n, h);
-        else if (__float_as_uint(acc[nt][mt].x) == 0x7fc00001u) act[m] = (LT)0;  // keep acc live
-        if (sv && !(YANERF_ABLATE & 4)) {
-          if constexpr (!PM && !GS)
-            pk_store_rows_b<T>((saved + (SR.h0 + 256LL * l + nrow0 + 16 * nt) * ld + p0),
-                               soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
+        pk_lds<T>(act, m, n, h);
+        if constexpr (sv) {
+          if constexpr (!PM && !GS)  // x3: feature-major rows from the epilogue
+            pk_store_rows_b<T>((saved + (SR.h0 + 256LL * l + nrow0 + 16 * nt) * ld + p0), soff, (int)ldb,
+                               16 * mt * (int)sizeof(ST), h);
           mask_acc(bits, h, nt * MT + mt);
         }
       }
@@ -1567,12 +1302,12 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
     if constexpr (PM) {
 #pragma unroll
       for (int w = 0; w < MW; ++w) pbits[w] = bits[w];
-    } else if (sv && !(YANERF_ABLATE & 4)) {
+    } else if constexpr (sv) {
 #pragma unroll
       for (int w = 0; w < MW; ++w)
         masks[((((int64_t)l * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane] = bits[w];
     }
-    if (!(YANERF_ABLATE & 32)) lds_barrier();
+    lds_barrier();
   }
   // ---- density head: sigma = w_d . h + b_d (nerf_mlp.py:173; density_layer 256->1) as one 16-row MFMA tile per
   // 16-point group (rows past 0 are zero weights); wave w takes groups w, w + WAVES, ...; lanes g == 0 hold sigma of
@@ -1583,25 +1318,23 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
   for (int hg = 0; hg < HG; ++hg) {
     const int grp = wave + hg * WAVES;
     sig[hg] = 0.f;
-    if (!(YANERF_ABLATE & 8) && grp < MT) {
+    if (grp < MT) {
       f4 hacc[1][1];
       gemm_lds<T, 1, 1>(Wt + lay.wdh_off, wpl, 256, 0, act + 16 * grp * ROW, 0, 256 / KB, hacc, lane);
       sig[hg] = hacc[0][0].x + Wf[lay.bd_off];
     }
   }
   // ---- intermediate_linear (no activation)
-  gemm_lds<T, NT, MT, GS ? YANERF_F32_GSAVE_POS_FWD : 0>(Wt + lay.wint_off, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, Wf + lay.bint_off, &ring,
-                          hsave(lay.L - 1));
+  gemm_lds<T, NT, MT, GS ? RSV_FWD : 0>(Wt + lay.wint_off, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane,
+                                        Wf + lay.bint_off, &ring, hsave(lay.L - 1));
   const int crow0 = wave * NTC * 16;
   ARing<T, NTC> ringc;
   ring_fill<T, NTC>(ringc, Wt + lay.wc_off, wpl, KC, crow0, KC / KB, lane);
-  if constexpr (PM) {
-    if (sv && !(YANERF_ABLATE & 4)) {
-      save_relu_pm<T, NTHR, 256>(act, 0, (char*)saved + PS.h0 + ((lay.L - 1) * Npad + p0) * 256LL * PM_HB, tid);
+  if constexpr (PM && sv) {
+    save_relu_pm<T, NTHR, 256>(act, 0, (char*)saved + PS.h0 + ((lay.L - 1) * Npad + p0) * 256LL * PM_HB, tid);
 #pragma unroll
-      for (int w = 0; w < MW; ++w)
-        masks[((((int64_t)(lay.L - 1) * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
-    }
+    for (int w = 0; w < MW; ++w)
+      masks[((((int64_t)(lay.L - 1) * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
   }
   lds_barrier();
   // fp8 Y: each wave's |max| of Y in the PE columns 32.. of row 16 (free once the trunk is done: the direction
@@ -1618,12 +1351,12 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
         const int m = 16 * mt + li;
         const Pk<T> h = pk_make<T>(v);
         pk_lds<T>(act, m, n, h);
-        if constexpr (PM && YANERF_BF16_Y8) gmax.add(h);
-        if (sv && !PM) pk_store_rows_b<T>((saved + (SR.y + nrow0 + 16 * nt) * ld + p0),
-                             soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
+        if constexpr (PM) gmax.add(h);
+        if constexpr (sv && !PM)
+          pk_store_rows_b<T>((saved + (SR.y + nrow0 + 16 * nt) * ld + p0), soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
       }
     }
-    if constexpr (PM && YANERF_BF16_Y8) {
+    if constexpr (PM) {
       static_assert(PE_COL + 32 + 2 * WAVES <= ROW, "Y scale slots");
       const float am = wave_max(gmax.value());
       if (sv && lane == 0) yred[wave] = am;
@@ -1633,21 +1366,18 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
   {
     const float nrm = fmaxf(sqrtf(d3[0] * d3[0] + d3[1] * d3[1] + d3[2] * d3[2]), 1e-12f);
     float dn[3] = {d3[0] / nrm, d3[1] / nrm, d3[2] / nrm};
-    if (!(YANERF_ABLATE & 2))
-      harmonic_to_lds<T>(act, mt_, PE_COL, KDIR, dn, lay.fd, lay.ad, q,
-                         (saved && !PM) ? saved + SR.dpe * ld + p : nullptr, ld);
+    harmonic_to_lds<T>(act, mt_, PE_COL, KDIR, dn, lay.fd, lay.ad, q, (saved && !PM) ? saved + SR.dpe * ld + p : nullptr,
+                       ld);
   }
   lds_barrier();
   // ---- color layer: LinearWithRepeat(256 + 27 -> 128) + ReLU as one K = 288 GEMM over [Y, dirPE]
   {
     f4 accc[NTC][MT];
     gemm_lds<T, NTC, MT>(Wt + lay.wc_off, wpl, KC, crow0, act, 0, KC / KB, accc, lane, Wf + lay.bc_off, &ringc);
-    if constexpr (PM) {
-      if (sv) {
-        save_grad_pm<T, NTHR, 256, YANERF_BF16_Y8>(act, (char*)saved + PS.y + p0 * 256 * PM_YB,
-                                                   (float*)((char*)saved + PS.ysc) + tile, yred, WAVES, tid);
-        copy_tile_pm<T, NTHR, KDIR>(act, PE_COL, (ST*)((char*)saved + PS.dpe) + p0 * KDIR, tid);
-      }
+    if constexpr (PM && sv) {
+      save_grad_pm<T, NTHR, 256>(act, (char*)saved + PS.y + p0 * 256 * PM_YB, (float*)((char*)saved + PS.ysc) + tile,
+                                 yred, WAVES, tid);
+      copy_tile_pm<T, NTHR, KDIR>(act, PE_COL, (ST*)((char*)saved + PS.dpe) + p0 * KDIR, tid);
     }
     lds_barrier();
 #pragma unroll
@@ -1660,7 +1390,7 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
         const int m = 16 * mt + li;
         const Pk<T> h = pk_make<T>(v);
         pk_lds<T>(act, m, n, h);
-        if (sv) {
+        if constexpr (sv) {
           if constexpr (!PM)
             pk_store_rows_b<T>((saved + (SR.c + crow0 + 16 * nt) * ld + p0), soff, (int)ldb,
                                16 * mt * (int)sizeof(ST), h);
@@ -1676,8 +1406,7 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
   for (int hg = 0; hg < HG; ++hg) {
     const int grp = wave + hg * WAVES;
     f4 hacc[1][1] = {{f4{0.f, 0.f, 0.f, 0.f}}};
-    if (!(YANERF_ABLATE & 8) && grp < MT)
-      gemm_lds<T, 1, 1>(Wt + lay.woh_off, wpl, HC, 0, act + 16 * grp * ROW, 0, HC / KB, hacc, lane);
+    if (grp < MT) gemm_lds<T, 1, 1>(Wt + lay.woh_off, wpl, HC, 0, act + 16 * grp * ROW, 0, HC / KB, hacc, lane);
     const int64_t pw = p0 + 16 * grp + li;
     if (grp < MT && g == 0 && pw < N) {
       sigma[pw] = sig[hg];
@@ -1691,22 +1420,17 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::WAVES * 64)
       }
     }
   }
-  if constexpr (PM) {
-    if (sv) save_relu_pm<T, NTHR, HC>(act, 0, (char*)saved + PS.c + p0 * (int64_t)HC * PM_HB, tid);  // C still in LDS
-  }
-  if (HALVES > 1 && YANERF_PP_SHIFT && half == 0) lds_barrier();  // the first half's extra barrier (it entered one segment early)
+  if constexpr (PM && sv) save_relu_pm<T, NTHR, HC>(act, 0, (char*)saved + PS.c + p0 * (int64_t)HC * PM_HB, tid);
 }
 
-// ---- the colour layer's direction columns by rays (YANERF_DIRPE_RAY). LinearWithRepeat (nerf_mlp.py) feeds every
+// ---- the colour layer's direction columns by rays (fp32). LinearWithRepeat (nerf_mlp.py) feeds every
 // point of a ray the same direction embedding, so dW_dir[c][k] = sum_p dZc[p][c] dirPE[ray(p)][k]
 // = sum_r dirPE[r][k] (sum_{p in r} dZc[p][c]). The dX kernel sums dZc per ray over each thread-chunk of its tile
 // (dzc_chunk points, ascending), the block kernel adds a ray's chunk partials (ascending) and accumulates the products
 // over blocks of DIRB rays (ascending), the final kernel adds the blocks (ascending): deterministic, and a 128 x 27
 // product over R rays replaces a 128 x 64 dW tile over every point. Used when P >= dzc_chunk (a ray then touches at
-// most two partials per chunk slot).
-#ifndef YANERF_DIRPE_RAY
-#define YANERF_DIRPE_RAY 1
-#endif
+// most two partials per chunk slot). fp32 only: its fine backward measured 15.2 -> 15.0 ms; bf16 and x3 gained less in
+// dW than the per-ray sums cost in their dX (bf16 1.76 -> 1.79 ms, x3 10.11 -> 10.15 ms).
 template <typename T> __host__ __device__ constexpr int dzc_chunk() { return Cfg<T>::M / (Cfg<T>::DXWAVES * 64 / HC); }
 constexpr int DIRB = 16;  // rays per block of the dirPE product
 template <typename T> __device__ __forceinline__ float lds_val(const typename Cfg<T>::lds_t* act, int m, int col);
@@ -1724,7 +1448,7 @@ template <> __device__ __forceinline__ float lds_val<x3_t>(const bf16_t* act, in
 
 // ============================================================================================ backward dX
 template <typename T>
-__global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
+__global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64)
     __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_bwd_dx_kernel(
     MlpLayout lay, const typename Cfg<T>::w_t* __restrict__ Wt, const float* __restrict__ Wf,
     const uint64_t* __restrict__ masks, const float* __restrict__ rgb, const float* __restrict__ g_sigma,
@@ -1741,18 +1465,12 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
   constexpr int KB = Cfg<T>::KB, TPP = WAVES * 64 / M, CPT = HC / TPP;  // colour columns per thread
   static_assert(CPT % 16 == 0, "colour-head backward: whole 16-feature tiles per thread");
   typedef typename Cfg<T>::lds_t LT;
-  // two point tiles per workgroup, the second half one barrier segment behind the first (as the forward, HALVES)
-  constexpr int HALVES = Cfg<T>::HALVES;
-  __shared__ __attribute__((aligned(16))) LT act_all[HALVES * Cfg<T>::PLANES * M * ROW];
-  const int half = HALVES > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x / (WAVES * 64)) : 0;
-  LT* const act = act_all + half * Cfg<T>::PLANES * M * ROW;
-  const int tid = HALVES > 1 ? (int)threadIdx.x & (WAVES * 64 - 1) : (int)threadIdx.x, lane = tid & 63;
+  __shared__ __attribute__((aligned(16))) LT act[Cfg<T>::PLANES * M * ROW];
+  const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
-  const int64_t tile = HALVES > 1 ? (int64_t)blockIdx.x * HALVES + half : (int64_t)blockIdx.x;
-  const int64_t ntiles = HALVES > 1 ? (int64_t)gridDim.x * HALVES : (int64_t)gridDim.x;
+  const int64_t tile = (int64_t)blockIdx.x, ntiles = (int64_t)gridDim.x;
   const int64_t p0 = tile * M;
-  if (HALVES > 1 && YANERF_PP_SHIFT && half == 1) lds_barrier();
   typedef typename Cfg<T>::st_t ST;
   const int64_t ld = row_ld(Npad, sizeof(ST)), ldb = ld * (int64_t)sizeof(ST);
   const uint32_t soff = (uint32_t)(4 * g * ldb + li * (int64_t)sizeof(ST));  // this lane's offset in a row tile
@@ -1769,7 +1487,7 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
   [[maybe_unused]] float* const g8scl = (float*)(gb + PG.scale) + tile;
   [[maybe_unused]] const int64_t ntile = Npad / M;
   auto g8_note = [&](int set, float amax) {  // this wave's |max| of the section being formed
-    if constexpr (PM && YANERF_BF16_G8) {
+    if constexpr (PM) {
       amax = wave_max(amax);
       if (lane == 0) g8red[8 * set + wave] = amax;
     }
@@ -1862,7 +1580,6 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
           // feature cl within its 16-feature tile: ballot word cl & 3, bit 16 * (cl >> 2) + point
           const bool on = (cw[t][cl & 3] >> (16 * (cl >> 2) + (mt_ & 15))) & 1ull;
           dz[e] = on ? dc[e] : 0.0f;
-          if constexpr ((YANERF_ABLATE & 64) != 0) dz[e] = (float)c;
           if constexpr (!PM) grad[(GR.dzc + c) * ld + p] = to_st<T>(dz[e]);
           amax = fmaxf(amax, fabsf(dz[e]));
         }
@@ -1901,10 +1618,9 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
     if (n > nb) dzc_part[(u * 2 + 1) * HC + c] = s1;
   }
   lds_barrier();
-  // fp32 (YANERF_F32_GSAVE_DX): dY and dZ_l (l >= 1) leave from the B fragments of the GEMM that reads them, each
-  // K-block's stores BEFORE its MFMAs (RSV 2; after them, as the forward does, measured slower here); dZ_0 from the
-  // last epilogue
-  constexpr bool GSX = std::is_same<T, float>::value && YANERF_F32_GSAVE_DX;
+  // fp32: dY and dZ_l (l >= 1) leave from the B fragments of the GEMM that reads them, each K-block's stores BEFORE its
+  // MFMAs (RSV_DX; after them, as the forward does, measured slower here); dZ_0 from the last epilogue
+  constexpr bool GSX = std::is_same<T, float>::value;
   G8Max gmax;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
@@ -1914,7 +1630,7 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
       const int m = 16 * mt + li;
       f4 v = acc[nt][mt];
       const Pk<T> h = pk_make<T>(v);
-      if constexpr (PM && YANERF_BF16_G8) gmax.add(h);
+      if constexpr (PM) gmax.add(h);
       pk_lds<T>(act, m, n, h);
       if constexpr (!PM && !GSX)  // else stored by the first trunk step's GEMM
         pk_store_rows_b<T>((grad + (GR.dyx + nrow0 + 16 * nt) * ld + p0),
@@ -1935,12 +1651,12 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
 #pragma unroll
     for (int w = 0; w < MW; ++w)
       bits[w] = masks[((((int64_t)hl * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane];
-    gemm_lds<T, NT, MT, GSX ? YANERF_F32_GSAVE_POS_DX : 0>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring,
-                             RowSave{(float*)(void*)(grad + (HEAD ? GR.dyx : GR.dz0 + 256LL * l) * ld + p0), soff,
-                                     (int)ldb, 256 / KB, wave, WAVES, p0 * 255 * (int64_t)sizeof(ST)});
+    gemm_lds<T, NT, MT, GSX ? RSV_DX : 0>(A, wpl, 256, nrow0, act, 0, 256 / KB, acc, lane, nullptr, &ring,
+                                          RowSave{(float*)(void*)(grad + (HEAD ? GR.dyx : GR.dz0 + 256LL * l) * ld + p0),
+                                                  soff, (int)ldb, 256 / KB, wave, WAVES});
     if (l - 1 >= 1) ring_fill<T, NT, true>(ring, Wt + lay.wt_off[l - 1], wpl, 256, nrow0, 256 / KB, lane);
     // fp8 scale sets: dZc 0, dY 1, then dZ_{L-1}, dZ_{L-2}, ... alternate from set 0
-    if constexpr (PM && !(YANERF_ABLATE & 128)) {  // the GEMM's input: dY (from the heads) or dZ_l
+    if constexpr (PM) {  // the GEMM's input: dY (from the heads) or dZ_l
       if constexpr (HEAD)
         save_grad_pm<T, NTHR, 256>(act, gb + PG.dy + p0 * 256 * PM_GB, g8scl + lay.L * ntile, g8red + 8, WAVES, tid);
       else
@@ -1964,11 +1680,12 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
         }
         // ReLU mask of H_{hl}: this lane's own bits of this tile (packed by the forward)
         const Pk<T> h = pk_make<T>(apply_mask_tile<T, MW>(v, bits, nt * MT + mt));
-        if constexpr (PM && YANERF_BF16_G8) gmax.add(h);
+        if constexpr (PM) gmax.add(h);
         pk_lds<T>(act, m, n, h);
-        if (!PM && (!GSX || hl == 0))
-          pk_store_rows_b<T>((grad + (GR.dz0 + 256LL * hl + nrow0 + 16 * nt) * ld + p0),
-                             soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
+        if constexpr (!PM)
+          if (!GSX || hl == 0)
+            pk_store_rows_b<T>((grad + (GR.dz0 + 256LL * hl + nrow0 + 16 * nt) * ld + p0), soff, (int)ldb,
+                               16 * mt * (int)sizeof(ST), h);
       }
     }
     g8_note((lay.L + 1 - hl) & 1, gmax.value());  // dZ_hl
@@ -1976,20 +1693,17 @@ __global__ void __launch_bounds__(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64)
   };
   trunk_step(std::integral_constant<bool, true>{}, lay.L);
   for (int l = lay.L - 1; l >= 1; --l) trunk_step(std::integral_constant<bool, false>{}, l);
-  if constexpr (PM && !(YANERF_ABLATE & 128))
+  if constexpr (PM)
     save_grad_pm<T, NTHR, 256>(act, gb + PG.dz0 + p0 * 256 * PM_GB, g8scl, g8red + 8 * ((lay.L + 1) & 1), WAVES, tid);
-  if (HALVES > 1 && YANERF_PP_SHIFT && half == 0) lds_barrier();
 }
 
 // ============================================================================================ backward dW
-// dW_l[n][k] = sum_points dZ_l[n][p] * X_l[k][p] (+ bias column: sum_points dZ_l[n][p]), both operands stored
-// feature-major ([row][point], written by the forward / dX kernels). One workgroup owns a [BN x 128] tile of
-// dW for a contiguous split of the points: per stage it stages 128-byte row segments (2 K-blocks) of the BN
-// dZ rows and the 128 X rows into LDS once (coalesced 16-B loads, next stage prefetched into registers while
-// the current one is multiplied), XOR-swizzled so the 16 rows a ds_read_b128 group touches hit distinct bank
-// slots; 8 waves tile the output (BN/64) x (8*64/BN). The bias gradient is a VALU row-sum of the staged dZ
-// rows in the k-tile-0 workgroups. Partial tiles go to per-split fp32 slabs; dw_reduce sums them in split
-// order (deterministic) straight into the reference-layout gradient tensors.
+// dW_l[n][k] = sum_points dZ_l[n][p] * X_l[k][p] (+ bias column: sum_points dZ_l[n][p]). One workgroup owns a
+// [BN x BK] tile of one layer's dW for a contiguous split of the points; partial tiles go to per-split fp32 slabs and
+// dw_reduce sums them in split order (deterministic, no atomics) straight into the reference-layout gradient tensors.
+// Three tile kinds: fp32 (dw_tile: feature-major rows staged by LDS-DMA, fp32 MFMA), bf16 (dw_tile_pm: point-major fp8 /
+// bf16 sections, transposed LDS reads, fp8 block-scaled or bf16 MFMA) and x3 (dw_tile_x3: fp32 rows split into three
+// bf16 planes on the way into LDS).
 struct DwJob {
   // (column / row counts are int16: the whole DwJobs block is a kernel argument and must stay within 4 KB)
   const void* A;  // dZ rows [a_rows][ld] (points contiguous)
@@ -2000,8 +1714,8 @@ struct DwJob {
   float* b;  // grad of bias [a_rows]
   const float* a_scale;  // A's decode scale per 128-point tile
   const float* x_scale;  // X0's decode scale per 128-point tile (fp8 Y), or null
-  // fp32 (YANERF_DW_FUSE_DENSITY): this job also forms a head's weight gradient in its tiles, into that head job's slab
-  // region at ext_slab_off (the head job then has no tiles of its own):
+  // fp32: this job also forms a head's weight gradient in its tiles, into that head job's slab region at ext_slab_off
+  // (the head job then has no tiles of its own):
   //  ext 1 (intermediate_linear): density -- the dsigma row (the gradient row right after the job's 256 A rows)
   //        against the job's own X = H_{L-1};
   //  ext 2 (color_layer.0, its first k-tile): color_layer.2 -- ext_rows dU rows (ext_a) against the 128 rows of C
@@ -2009,8 +1723,7 @@ struct DwJob {
   int64_t ext_slab_off;
   const void* ext_a;
   const void* ext_x;
-  int wg_base;  // first workgroup of the job in the 1-D grid
-  int16_t tS[4];  // point splits of each k-tile (equal unless the split plan balances the grid, dw_plan)
+  int wg_base;  // first workgroup of the job in the 1-D grid (k_tiles * S workgroups per job)
   int16_t a_rows;
   int16_t x0_rows;
   int16_t x1_rows;
@@ -2024,8 +1737,8 @@ struct DwJob {
   // padded to x0p (a multiple of 8), then X1's (ktot_v = x0p + x1_rows); k-tiles are laid over ktot_v
   int16_t a_ld, a_chunks, x0_ld, x1_ld, x0p, ktot_v;
   int16_t w_ld;  // row stride of W: ktot, or more when trailing columns come from elsewhere (the per-ray dirPE term)
-  int16_t x0_u8, x1_u8;  // X0 / X1 stored as fp8 e4m3 (YANERF_BF16_A8: the post-ReLU sections); a k-tile is one format
-  int16_t a_u8;          // A stored as fp8 e4m3 of value / scale (YANERF_BF16_G8: dZ_l, dY, dZc; not dU)
+  int16_t x0_u8, x1_u8;  // X0 / X1 stored as fp8 e4m3 (the post-ReLU sections, Y); a k-tile is one format
+  int16_t a_u8;          // A stored as fp8 e4m3 of value / scale (dZ_l, dY, dZc; not dU)
   int16_t ext, ext_rows, ext_ktot;
   int16_t gi;  // index of the job's weight gradient in the parameter list (2 * layer, ...)
 };
@@ -2034,9 +1747,8 @@ struct DwJobs {
   DwJob j[kMaxDwJobs];
   int n;
   int total_tiles;
-  int total_wg;  // workgroups of the dW launch (sum over k-tiles of their point splits)
-  int s_uniform; // the split count of every k-tile when they are all equal (dw_plan), else 0
-  int bkmax;     // dw_bkmax of the precision (the reduce maps a column to its k-tile)
+  int total_wg;  // workgroups of the dW launch (total_tiles * S)
+  int S;         // point splits of every k-tile
   int64_t slab_elems;
   int64_t slab_stride;  // elements between two splits' slabs: slab_elems padded to a multiple of 4 (dw_slab_pad)
 };
@@ -2048,99 +1760,58 @@ template <typename T> constexpr int prec_of = YANERF_PREC_BF16;
 template <> constexpr int prec_of<float> = YANERF_PREC_F32;
 template <> constexpr int prec_of<x3_t> = YANERF_PREC_F32X3;
 
+__device__ __forceinline__ float hsum4(f4 v) { return (v.x + v.y) + (v.z + v.w); }
 
-template <typename T> __device__ __forceinline__ float hsum16(f4 v);
-template <> __device__ __forceinline__ float hsum16<float>(f4 v) { return (v.x + v.y) + (v.z + v.w); }
-// bf16: the 8 halves widened exactly (a bf16 is the high half of an fp32) and summed in fp32. (A dot2-with-ones form,
-// __builtin_amdgcn_fdot2_f32_bf16, was miscompiled by this toolchain: the four v_dot2c_f32_bf16 all read the first
-// dword, so every bf16 bias gradient was wrong; caught by tests/test_gpu_parity.py::test_mlp_bf16_gradients_elementwise.)
-template <> __device__ __forceinline__ float hsum16<bf16_t>(f4 v) {
-  const uint32_t u[4] = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-  float s[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) s[i] = __uint_as_float(u[i] << 16) + __uint_as_float(u[i] & 0xffff0000u);
-  return (s[0] + s[1]) + (s[2] + s[3]);
-}
-
-// Stage ring: DW_STAGES buffers of up to 512 rows x 64 B (one K-block of points per row), filled by LDS-DMA
-// (global_load_lds_dwordx4; one wave-instruction = 16 whole rows) DW_STAGES-1 stages ahead of the one being
+// fp32 stage ring: DW32_STAGES buffers of up to 392 rows x 128 B (two K-blocks = 32 points per row), filled by LDS-DMA
+// (global_load_lds_dwordx4; one wave-instruction = 8 whole rows) DW32_STAGES - 1 stages ahead of the one being
 // multiplied. The DMA destination is lane-linear, so the bank swizzle (16-byte chunk c of row r stored at
-// c ^ (2 * ((r >> 3) & 1)), conflict-free for the 16x16 fragment reads) goes on the SOURCE chunk. One raw barrier
-// per stage: after it every wave's DMA for this stage has landed (each wave waited for its own with a counted
-// vmcnt) and every wave is done reading the buffer the next DMA overwrites.
-// fp32 dW: two K-blocks (32 points) per stage in a 3-deep ring of 48 KB stages: half the stage barriers of one
-// K-block per stage (round 2, with the two-K-block stagger below: 7.98 -> 7.86 ms). The x3 dW keeps its own 64-byte
-// rows (dw_swz4).
-#ifndef YANERF_DW_CPR
-#define YANERF_DW_CPR 8
-#endif
-constexpr int DW_CPR = YANERF_DW_CPR;      // 16-byte chunks per staged row (4: one K-block, 8: two)
-constexpr int DW_RB = 16 * DW_CPR;          // staged row bytes
-constexpr int DW_RPI = 64 / DW_CPR;         // rows per DMA wave-instruction
-#ifndef YANERF_DW_PF
-#define YANERF_DW_PF 0
-#endif
-constexpr bool DW_PF = YANERF_DW_PF;  // fp32 dW: prefetch the next stage's fragments during the current MFMAs
-#ifndef YANERF_DW_STAGGER
-#define YANERF_DW_STAGGER 1
-#endif
-constexpr int DW_STAGGER = YANERF_DW_STAGGER;  // fp32 dW: SIMD partners staggered (2: + setprio 1 for waves 4-7)
-#ifndef YANERF_DW_ORDER
-#define YANERF_DW_ORDER 1
-#endif
-constexpr bool DW_ORDER = YANERF_DW_ORDER;  // fp32 dW: row-fragment-outer MFMA order (early first MFMA)
-#ifndef YANERF_DW_STAGES
-#define YANERF_DW_STAGES (YANERF_DW_CPR == 4 ? 4 : 2)
-#endif
-constexpr int DW_STAGES = YANERF_DW_STAGES, DW_STAGE_BYTES = 512 * DW_RB;
-// fp32 ring: a stage holds at most 256 + 128 rows (dw_bkmax 128): 3 stages of 48 KB (two K-blocks per row) = 144 KB,
-// or with one K-block per row 4 stages of 24 KB = 96 KB. (With one K-block, 3 stages = 72 KB let two workgroups share
-// a CU -- 16 waves, 4 per SIMD, at the tile's 116 VGPRs -- and measured slower: fp32 dW 8.15 -> 8.33 ms; the fp32
-// dW's idle MFMA cycles are not stage-barrier bubbles another workgroup could fill.)
-#ifndef YANERF_DW32_STAGES
-#define YANERF_DW32_STAGES (YANERF_DW_CPR == 4 ? 4 : 3)
-#endif
-template <typename T> struct DwRing {
-  static constexpr int STAGES = DW_STAGES, STAGE_BYTES = DW_STAGE_BYTES;
-};
+// c ^ ((r >> 1) & 7), conflict-free for the 16x16 fragment reads) goes on the SOURCE chunk. One raw barrier per stage:
+// after it every wave's DMA for this stage has landed (each wave waited for its own with a counted vmcnt) and every wave
+// is done reading the buffer the next DMA overwrites. Two K-blocks per stage halve the stage barriers of one K-block
+// per stage (round 2, with the stagger below: 7.98 -> 7.86 ms). A stage holds at most 256 + 128 rows (dw_bkmax 128) +
+// DW_EXT_ROWS: 3 stages of 49 KB. (Smaller rings so two workgroups share a CU measured slower: the fp32 dW's idle MFMA
+// cycles are not stage-barrier bubbles another workgroup could fill.)
+constexpr int DW_CPR = 8;           // 16-byte chunks per staged row
+constexpr int DW_RB = 16 * DW_CPR;  // staged row bytes
+constexpr int DW_RPI = 64 / DW_CPR; // rows per DMA wave-instruction
+constexpr int DW32_STAGES = 3;
 // + DW_EXT_ROWS rows per stage for a fused head (one DMA wave-instruction of A rows: the dsigma row or the dU rows,
-// then spare rows); the colour tile (128 + 128 rows) stages C's 128 rows beside them in the same 392-row stage
+// then spare rows); the colour tile (128 + 128 rows) stages C's 128 rows beside them in the same 392-row stage. The
+// heads' weight gradients inside the bigger tiles: the density and colour-output jobs, as 64-row tiles with one / three
+// useful rows, took 0.42 ms of the 7.6 ms fine fp32 dW (fused: 7.65 -> 7.39 ms, bitwise equal).
 constexpr int DW_EXT_ROWS = 8;
-template <> struct DwRing<float> {
-  static constexpr int STAGES = YANERF_DW32_STAGES, STAGE_BYTES = (256 + 128 + DW_EXT_ROWS) * DW_RB;
-};
-// fp32 dW: the density layer's weight gradient (one output row) formed inside the intermediate_linear tiles, which
-// stage its operand H_{L-1} anyway (an extra 16-row MFMA tile holding the dsigma row, one accumulator per wave), instead
-// of a 64-row tile with one useful row that stages H_{L-1} a second time (measured: the density and colour-output jobs
-// take 0.42 ms of the 7.6 ms fine fp32 dW). Bitwise the same density gradient (same per-accumulator point order).
-#ifndef YANERF_DW_FUSE_DENSITY
-#define YANERF_DW_FUSE_DENSITY 1
-#endif
-// points per dW stage: one K-block of the dW MFMA per staged row (x3: always one bf16 K-block, register staged)
-constexpr int X3_SPTS = 32;
+constexpr int DW32_STAGE_BYTES = (256 + 128 + DW_EXT_ROWS) * DW_RB;
+// points per dW stage
+constexpr int X3_SPTS = 32;   // x3: one bf16 K-block, register staged
+constexpr int PM_SPTS = 64;   // bf16: two stacked 32-point K-blocks per LDS-DMA stage (half the stage barriers)
 static int64_t dw_stage_pts(int prec) {
   if (prec == YANERF_PREC_F32X3) return X3_SPTS;
-  if (prec == YANERF_PREC_BF16 && YANERF_BF16_PM) return YANERF_PM_SPTS;
-  return (prec == YANERF_PREC_F32 ? Cfg<float>::KB : Cfg<bf16_t>::KB) * (DW_CPR / 4);
+  if (prec == YANERF_PREC_BF16) return PM_SPTS;
+  return Cfg<float>::KB * (DW_CPR / 4);
 }
-__device__ __forceinline__ int dw_swz4(int row, int c) { return c ^ (((row >> 3) & 1) << 1); }  // 64-byte rows
-__device__ __forceinline__ int dw_swz(int row, int c) { return DW_CPR == 4 ? dw_swz4(row, c) : (c ^ ((row >> 1) & 7)); }
+__device__ __forceinline__ int dw_swz4(int row, int c) { return c ^ (((row >> 3) & 1) << 1); }  // 64-byte rows (x3)
+__device__ __forceinline__ int dw_swz(int row, int c) { return c ^ ((row >> 1) & 7); }          // 128-byte rows
 
-template <typename T, int BN, int BK, int EXT = 0>
+// fp32 dW tile. Staggered SIMD partners: a 512-thread workgroup puts waves w and w + 4 on one SIMD; waves 4-7 multiply
+// the previous stage's second K-block (kept in registers) and then this stage's first, waves 0-3 both K-blocks of this
+// stage, so while one partner waits on its LDS reads after the stage barrier the other has MFMAs ready (round 2:
+// 8.15 -> 7.95 ms). Per accumulator the points still arrive in order: bitwise equal to the unstaggered loop.
+template <int BN, int BK, int EXT = 0>
 __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, int64_t Npad, float* __restrict__ slab,
                                         int64_t slab_elems, char* smem) {
+  typedef float T;
   constexpr int EPC = Cfg<T>::EPC, KB = Cfg<T>::KB;
-  constexpr int RSTG = DwRing<T>::STAGES, RSB = DwRing<T>::STAGE_BYTES;  // ring depth, bytes per stage
+  constexpr int RSTG = DW32_STAGES, RSB = DW32_STAGE_BYTES;  // ring depth, bytes per stage
   constexpr int WN = BN / 64, WK0 = 8 / WN, WK = (BK / 16 < WK0) ? BK / 16 : WK0, KTW = BK / WK / 16;
   static_assert(KTW >= 1 && WN * WK <= 8, "dW wave tiling");
   // EXT: DW_EXT_ROWS head A rows after the X rows (rows XE ..), then (EXT 2) the head's 128 X rows (rows XX ..)
   constexpr int XE = BN + BK, XX = XE + DW_EXT_ROWS, XH = EXT == 2 ? 128 : 0;
   constexpr int ROWS = BN + BK + (EXT ? DW_EXT_ROWS + XH : 0), PW = (ROWS + 8 * DW_RPI - 1) / (8 * DW_RPI);
   static_assert((ROWS + DW_RPI - 1) / DW_RPI * DW_RPI * DW_RB <= RSB, "dW stage buffer");
-  static_assert(EXT == 0 || (std::is_same<T, float>::value && BK == 128 && DW_CPR == 8 && DW_STAGGER &&
-                             ((EXT == 1 && BN == 256) || (EXT == 2 && BN == 128))),
-                "fused heads: fp32 256 x 128 (density) / 128 x 128 (colour output) tiles, staggered two-K-block stages");
-  constexpr int KBS = DW_CPR / 4;                                             // K-blocks per stage
+  static_assert(EXT == 0 || (BK == 128 && ((EXT == 1 && BN == 256) || (EXT == 2 && BN == 128))),
+                "fused heads: fp32 256 x 128 (density) / 128 x 128 (colour output) tiles");
+  constexpr int KBS = DW_CPR / 4;  // K-blocks per stage
+  static_assert(KBS == 2, "the staggered loop below takes two K-blocks per stage");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
@@ -2199,81 +1870,14 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
 #pragma unroll
     for (int i = 0; i < BPT; ++i) {
       const int idx = tid + DW_THREADS * i, row = idx / DW_CPR, ch = idx % DW_CPR;
-      if (row < BN) rsum[i] += hsum16<T>(*(const f4*)(buf + row * DW_RB + (ch << 4)));
+      if (row < BN) rsum[i] += hsum4(*(const f4*)(buf + row * DW_RB + (ch << 4)));
     }
     if constexpr (EXT != 0) {
       if (tid < DW_CPR * J.ext_rows)
-        rsum_e += hsum16<T>(*(const f4*)(buf + (XE + tid / DW_CPR) * DW_RB + ((tid % DW_CPR) << 4)));
+        rsum_e += hsum4(*(const f4*)(buf + (XE + tid / DW_CPR) * DW_RB + ((tid % DW_CPR) << 4)));
     }
   };
-  if constexpr (DW_PF && KBS == 1) {
-    // Fragment prefetch: the wave reads stage st+1's MFMA fragments from LDS while it multiplies stage st's (held
-    // in registers since the previous iteration), so no stage starts on an LDS read latency. Stage st+1 must have
-    // landed at iteration st's barrier; the DMA issued after it (stage st + RSTG - 1) fills buffer
-    // (st-1) % RSTG, whose fragments were read at iteration st-2 and whose bias rows at iteration st-1.
-    static_assert(RSTG >= 3, "prefetch ring");
-    constexpr int NB = KTW;
-    f4 a[2][4], b[2][NB];
-    auto read_frags = [&](const char* buf, f4 (&fa)[4], f4 (&fb)[NB]) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int row = wn * 64 + 16 * nt + li;
-        fa[nt] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, g) << 4));
-      }
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const int row = BN + (wk * KTW + q) * 16 + li;
-        fb[q] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, g) << 4));
-      }
-    };
-    // wait until this wave's DMA of a stage has landed, given how many stages were issued after it
-    auto wait_dma = [&](int64_t after) {
-      if (after >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * 3) : "memory");
-      else if (after == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * 2) : "memory");
-      else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    };
-    auto mma = [&](const f4 (&fa)[4], const f4 (&fb)[NB]) {
-      if (!mma_wave) return;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-          for (int q = 0; q < NB; ++q)
-            acc[nt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[nt][ks], fb[q][ks], acc[nt][q], 0, 0, 0);
-    };
-    int64_t ihi = st_lo;  // next stage to issue
-#pragma unroll
-    for (int i = 0; i < RSTG - 1; ++i)
-      if (ihi < st_hi) issue(ihi++);
-    if (st_lo < st_hi) {
-      wait_dma(ihi - 1 - st_lo);
-      __builtin_amdgcn_s_barrier();
-      if (mma_wave) read_frags(smem + (int)(st_lo % RSTG) * RSB, a[0], b[0]);
-    }
-    // two stages per trip so the fragment buffers alternate without register copies
-    for (int64_t st = st_lo; st < st_hi; st += 2) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int64_t sc = st + h;
-        if (sc < st_hi) {
-          const bool has_next = sc + 1 < st_hi;
-          if (has_next) wait_dma(ihi - 1 - (sc + 1));
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-          if (ihi < st_hi) issue(ihi++);
-          if (has_next && mma_wave) read_frags(smem + (int)((sc + 1) % RSTG) * RSB, a[h ^ 1], b[h ^ 1]);
-          mma(a[h], b[h]);
-          if (do_bias) bias_rows(smem + (int)(sc % RSTG) * RSB);
-        }
-      }
-    }
-  } else if constexpr (DW_STAGGER && sizeof(T) == 4 && KBS == 2) {
-    // Two K-blocks per stage (YANERF_DW_CPR = 8: half the stage barriers), staggered by one K-block: waves 4-7 multiply
-    // the previous stage's second K-block (kept in registers) and then this stage's first, waves 0-3 both K-blocks of
-    // this stage. Per accumulator the points still arrive in order: bitwise equal to the unstaggered loop with the same
-    // stage size.
+  {
     const bool late = wave >= 4;
     f4 a0[4], b0[KTW], a1[2][4], b1[2][KTW];
     // EXT: the extra 16-row A fragment (the head rows first; rows past the staged 8 read whatever LDS holds there --
@@ -2373,180 +1977,6 @@ __device__ __forceinline__ void dw_tile(const DwJob& J, int k0, int s, int S, in
         if (do_bias) bias_rows(buf);
       }
     }
-  } else if constexpr (DW_STAGGER && sizeof(T) == 4 && KBS == 1) {
-    // Staggered SIMD partners (waves w and w + 4 share a SIMD). Both read stage st's fragments right after its
-    // barrier; waves 0-3 multiply k-steps 0..3 of stage st, waves 4-7 first finish k-steps 2..3 of stage st-1 from
-    // the registers they kept, then k-steps 0..1 of stage st. So while one partner waits on its LDS reads after the
-    // barrier the other has MFMAs ready. Every accumulator still sees its points in the same order (stage by stage,
-    // k-step by k-step): results are bitwise those of the unstaggered loop. LDS buffer lifetimes are unchanged (a
-    // stage's fragments are read in the segment after its barrier).
-    const bool late = wave >= 4;
-    if constexpr (DW_STAGGER == 2) {
-      if (late) __builtin_amdgcn_s_setprio(1);
-    }
-    f4 a[2][4], b[2][KTW];
-    auto read_frags = [&](const char* buf, f4 (&fa)[4], f4 (&fb)[KTW]) {
-#pragma unroll
-      for (int q = 0; q < KTW; ++q) {
-        const int row = BN + (wk * KTW + q) * 16 + li;
-        fb[q] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, g) << 4));
-      }
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int row = wn * 64 + 16 * nt + li;
-        fa[nt] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, g) << 4));
-      }
-    };
-    auto half = [&](const f4 (&fa)[4], const f4 (&fb)[KTW], int ks0) {
-#pragma unroll
-      for (int ks = ks0; ks < ks0 + 2; ++ks)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-          for (int q = 0; q < KTW; ++q)
-            acc[nt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[nt][ks], fb[q][ks], acc[nt][q], 0, 0, 0);
-    };
-#pragma unroll
-    for (int i = 0; i < RSTG - 1; ++i)
-      if (st_lo + i < st_hi) issue(st_lo + i);
-    auto begin_stage = [&](int64_t sc) {
-      const int64_t ahead = st_hi - 1 - sc;
-      static_assert(RSTG >= 2 && RSTG <= 5, "wait ladder below");
-      if (ahead >= RSTG - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (RSTG - 2)) : "memory");
-      else if (RSTG == 5 && ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * 2) : "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (sc + RSTG - 1 < st_hi) issue(sc + RSTG - 1);
-      return (const char*)(smem + (int)(sc % RSTG) * RSB);
-    };
-    // Separate straight-line loops per role (no branch between a stage's fragment reads and its MFMAs, so the
-    // compiler's lgkmcnt wait lands right before the first MFMA that uses the new fragments).
-    if (late && mma_wave) {
-      if (st_lo < st_hi) {
-        const char* buf = begin_stage(st_lo);
-        read_frags(buf, a[0], b[0]);
-        half(a[0], b[0], 0);
-        if (do_bias) bias_rows(buf);
-      }
-      // two stages per trip so the fragment sets alternate without register copies
-      for (int64_t st = st_lo + 1; st < st_hi; st += 2) {
-#pragma unroll
-        for (int h = 1; h >= 0; --h) {
-          const int64_t sc = st + (1 - h);
-          if (sc < st_hi) {
-            const char* buf = begin_stage(sc);
-            read_frags(buf, a[h], b[h]);
-            half(a[h ^ 1], b[h ^ 1], 2);
-            half(a[h], b[h], 0);
-            if (do_bias) bias_rows(buf);
-          }
-        }
-      }
-      if (st_hi > st_lo) {
-        if (((st_hi - 1 - st_lo) & 1) == 0) half(a[0], b[0], 2);
-        else half(a[1], b[1], 2);
-      }
-    } else {
-      for (int64_t sc = st_lo; sc < st_hi; ++sc) {
-        const char* buf = begin_stage(sc);
-        if (mma_wave) {
-          read_frags(buf, a[0], b[0]);
-          if constexpr (DW_ORDER) {
-            // row-fragment-outer: the first MFMAs need the column fragments and one row fragment
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-              for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-                for (int q = 0; q < KTW; ++q)
-                  acc[nt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0][nt][ks], b[0][q][ks], acc[nt][q], 0, 0, 0);
-          } else {
-            half(a[0], b[0], 0);
-            half(a[0], b[0], 2);
-          }
-        }
-        if (do_bias) bias_rows(buf);
-      }
-    }
-    if constexpr (DW_STAGGER == 2) {
-      if (late) __builtin_amdgcn_s_setprio(0);
-    }
-  } else {
-#pragma unroll
-  for (int i = 0; i < RSTG - 1; ++i)
-    if (st_lo + i < st_hi) issue(st_lo + i);
-  for (int64_t st = st_lo; st < st_hi; ++st) {
-    // my DMA for stage st is complete once at most the later issued stages remain outstanding
-    const int64_t ahead = st_hi - 1 - st;  // stages issued after st (at most RSTG - 2 here)
-    static_assert(RSTG >= 2 && RSTG <= 5, "wait ladder below");
-    if (ahead >= RSTG - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * (RSTG - 2)) : "memory");
-    else if (RSTG == 5 && ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW * 2) : "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (!(YANERF_ABLATE & 1024)) __builtin_amdgcn_s_barrier();
-    if (!(YANERF_ABLATE & 512) && st + RSTG - 1 < st_hi) issue(st + RSTG - 1);
-    const char* buf = smem + (int)(st % RSTG) * RSB;
-#pragma unroll
-    for (int kb = 0; kb < KBS; ++kb)
-    if (DW_ORDER && sizeof(T) == 4 && mma_wave) {
-      // column fragments first, then one row fragment per 4 x KTW MFMA group: the first MFMAs wait for KTW + 1 of the
-      // KTW + 4 reads, not all of them (same per-accumulator k order, bitwise equal)
-      f4 a[4], b[KTW];
-#pragma unroll
-      for (int q = 0; q < KTW; ++q) {
-        const int row = BN + (wk * KTW + q) * 16 + li;
-        b[q] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, kb * 4 + g) << 4));
-      }
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int row = wn * 64 + 16 * nt + li;
-        a[nt] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, kb * 4 + g) << 4));
-      }
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-          for (int q = 0; q < KTW; ++q)
-            acc[nt][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[nt][ks], b[q][ks], acc[nt][q], 0, 0, 0);
-    } else if (mma_wave) {
-      f4 a[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int row = wn * 64 + 16 * nt + li;
-        a[nt] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, kb * 4 + g) << 4));
-      }
-      // columns in groups of (at most) 4 tiles to bound the live fragment registers
-      constexpr int QG = KTW < 4 ? KTW : 4;
-#pragma unroll
-      for (int q0 = 0; q0 < KTW; q0 += QG) {
-        f4 b[QG];
-#pragma unroll
-        for (int q = 0; q < QG; ++q) {
-          const int row = BN + (wk * KTW + q0 + q) * 16 + li;
-          b[q] = *(const f4*)(buf + row * DW_RB + (dw_swz(row, kb * 4 + g) << 4));
-        }
-        if constexpr (sizeof(T) == 4) {
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-              for (int q = 0; q < QG; ++q)
-                acc[nt][q0 + q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[nt][ks], b[q][ks], acc[nt][q0 + q], 0, 0, 0);
-        } else {
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-            for (int q = 0; q < QG; ++q) acc[nt][q0 + q] = mma_blk<T>(a[nt], b[q], acc[nt][q0 + q]);
-        }
-      }
-    }
-    if (do_bias) bias_rows(buf);
-  }
   }
   float* out = slab + (int64_t)s * slab_elems + J.slab_off;
   const int kv = J.ktot + 1;
@@ -2609,19 +2039,12 @@ __device__ __forceinline__ int pm_swz(int r) {
   if constexpr (ROWB == 128) return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
   else return 2 * ((r & 3) | (((r >> 3) & 1) << 2));
 }
-constexpr int PM_SPTS = YANERF_PM_SPTS;  // points per dW stage: one or two 32-point K-blocks (images stacked)
-constexpr int PM_KBS = PM_SPTS / 32;
-static_assert(PM_SPTS == 32 || PM_SPTS == 64, "pm dW stage: 32 or 64 points");
-// stage buffer: the widest image pair (A + X, 32 points) of any instantiation
-#ifndef YANERF_PM_STAGE_KB
-#define YANERF_PM_STAGE_KB ((YANERF_BF16_G8 ? (YANERF_BF16_Y8 ? 16 : 24) : 32) * PM_KBS)
-#endif
-constexpr int PM_STAGE_BYTES = YANERF_PM_STAGE_KB * 1024;
-// LDS-DMA ring depth of the point-major (bf16) dW tile: as many stages as fit 128 KB
-#ifndef YANERF_PM_STAGES
-#define YANERF_PM_STAGES (128 / YANERF_PM_STAGE_KB)
-#endif
-constexpr int PM_STAGES = YANERF_PM_STAGES;
+constexpr int PM_KBS = PM_SPTS / 32;  // 32-point K-blocks per stage (images stacked)
+// stage buffer: the widest image pair (A + X, 64 points) of any instantiation (256-row fp8 A + 256-column fp8 X)
+constexpr int PM_STAGE_BYTES = 32 * 1024;
+// LDS-DMA ring depth of the point-major (bf16) dW tile: as many stages as fit 128 KB (2 / 3 stages so that two
+// workgroups could share a CU measured flat)
+constexpr int PM_STAGES = 4;
 // wait until this wave's DMA of the stage about to be read has landed, given how many stages it issued after that
 // one: vmcnt(PW * min(ahead, MAXA)) (the count must be an immediate)
 template <int PW, int MAXA>
@@ -2682,15 +2105,13 @@ __device__ __forceinline__ f4 pm_frag8(const char* img, int f0, int lane, float 
   return out;
 }
 
-// fp8 x fp8 tiles on the block-scaled fp8 MFMA (YANERF_DW_F8MMA): a 64-point stage is ONE
+// fp8 x fp8 tiles on the block-scaled fp8 MFMA: a 64-point stage is ONE
 // v_mfma_scale_f32_32x32x64_f8f6f4 per 32 x 32 output tile (e4m3 operands, 64 cycles: twice the bf16 rate, and no
 // widening), with the stage's power-of-two tile scales as the operands' e8m0 scales (exact, like the widening they
 // replace). Operand map (tools/probes/probe_mfma_f8.hip, exact on the MI355X): lane l holds A[row l % 32][k = 32 (l / 32)
 // + j] and B[k = 32 (l / 32) + j][col l % 32] in byte j of its 8 dwords. With points as k, lane (g, i) of a 16-lane group
-// needs points 32 (g >> 1) + 0..31 of feature 16 (g & 1) + i: four ds_read_b64_tr_b8 (8 points each).
-#ifndef YANERF_DW_F8MMA
-#define YANERF_DW_F8MMA 1
-#endif
+// needs points 32 (g >> 1) + 0..31 of feature 16 (g & 1) + i: four ds_read_b64_tr_b8 (8 points each). Fine dW
+// 1.06 -> 0.87 ms against the bf16 MFMA on widened operands (round 2).
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 // image swizzle for those reads: a 32-lane half touches 8 consecutive rows x the chunk pair (c0, c0 ^ 1), c0 even, so
@@ -2721,7 +2142,7 @@ __device__ __forceinline__ i32x8 f8m_frag(const char* img, int f0, int lane) {
 __device__ __forceinline__ int e8m0_of(float s) { return (int)((__float_as_uint(s) >> 23) & 0xffu); }
 template <int BN, int BK, bool X8, bool A8>
 constexpr bool use_f8mma() {
-  return YANERF_DW_F8MMA && X8 && A8 && BK == 256 && (BN == 256 || BN == 128) && YANERF_PM_SPTS == 64;
+  return X8 && A8 && BK == 256 && (BN == 256 || BN == 128) && PM_SPTS == 64;
 }
 
 template <int BN, int BK, bool X8, bool A8>
@@ -2964,12 +2385,8 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
 // current one multiplies), split into three bf16 planes on the way into LDS (same 64-byte rows and swizzle as the
 // bf16 dW tile) and multiplied with the six plane products per 16x16x32 step. Two LDS buffers, one barrier per
 // stage. Bias gradients are fp32 row sums of the loaded dZ segments.
-// x3 dW: software-pipelined staging (1) or split-then-multiply per stage (0). Measured equal (round 3,
-// profiles/r3_ab_x3_dw_pipe.jsonl: 5.41 / 5.42 vs 5.41 / 5.40 ms, bitwise-equal gradients): the split is not what
-// the x3 dW waits on
-#ifndef YANERF_X3_DWPIPE
-#define YANERF_X3_DWPIPE 0
-#endif
+// (A software-pipelined variant -- the next stage split while this one multiplies -- measured equal, round 3: the split
+// is not what the x3 dW waits on.)
 template <int BN, int BK>
 __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S, int64_t Npad,
                                            float* __restrict__ slab, int64_t slab_elems, char* smem) {
@@ -3035,64 +2452,6 @@ __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S,
       *(u32x2*)(buf + 2 * PLB + dst[i]) = u32x2{h2.w0, h2.w1};
     }
   };
-  if constexpr (YANERF_X3_DWPIPE) {
-    // software-pipelined stages: while a wave multiplies stage st from one buffer it splits stage st + 1 (loaded during
-    // stage st - 1) into the other, one staged segment after each of the six product terms, and reloads that segment's
-    // registers with stage st + 2 right away; one barrier per stage. (Unpipelined, every wave split its segments
-    // between two barriers with no MFMA in flight on its SIMD.) Each accumulator still sees the stages in order and the
-    // same six terms per stage: gradients bitwise equal.
-    static_assert(LPT <= 6, "x3 dW pipeline: one staged segment per product term");
-    if (st_lo < st_hi) {
-      load(st_lo);
-#pragma unroll
-      for (int i = 0; i < LPT; ++i) split_one(i, smem + (int)(st_lo & 1) * BUFB);
-      if (st_lo + 1 < st_hi) load(st_lo + 1);
-    }
-    __syncthreads();
-    for (int64_t st = st_lo; st < st_hi; ++st) {
-      char* buf = smem + (int)(st & 1) * BUFB;
-      char* nbuf = smem + (int)((st + 1) & 1) * BUFB;
-      const bool nxt = st + 1 < st_hi, nxt2 = st + 2 < st_hi;
-      if (mma_wave) {
-        f4 a[3][4];
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
-            const int row = wn * 64 + 16 * nt + li;
-            a[pl][nt] = *(const f4*)(buf + pl * PLB + row * 64 + (dw_swz4(row, g) << 4));
-          }
-        static_assert(KTW <= 4, "x3 dW pipeline: one column-fragment group");
-        f4 b[3][KTW];
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-          for (int q = 0; q < KTW; ++q) {
-            const int row = BN + (wk * KTW + q) * 16 + li;
-            b[pl][q] = *(const f4*)(buf + pl * PLB + row * 64 + (dw_swz4(row, g) << 4));
-          }
-        constexpr int TI[6] = {2, 1, 0, 1, 0, 0}, TJ[6] = {0, 1, 2, 0, 1, 0};
-#pragma unroll
-        for (int t = 0; t < 6; ++t) {
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-            for (int q = 0; q < KTW; ++q) acc[nt][q] = mma_blk<bf16_t>(a[TI[t]][nt], b[TJ[t]][q], acc[nt][q]);
-          if (t < LPT) {
-            if (nxt) split_one(t, nbuf);
-            if (nxt2) regs[t] = *(const f4*)(src[t] + (st + 2) * X3_SPTS);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < LPT; ++i) {
-          if (nxt) split_one(i, nbuf);
-          if (nxt2) regs[i] = *(const f4*)(src[i] + (st + 2) * X3_SPTS);
-        }
-      }
-      __syncthreads();
-    }
-  } else {
   if (st_lo < st_hi) load(st_lo);
   for (int64_t st = st_lo; st < st_hi; ++st) {
     char* buf = smem + (int)(st & 1) * BUFB;
@@ -3131,7 +2490,6 @@ __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S,
               acc[nt][q0 + q] = mma_blk<bf16_t>(a[TI[t]][nt], b[TJ[t]][q], acc[nt][q0 + q]);
       }
     }
-  }
   }
   float* out = slab + (int64_t)s * slab_elems + J.slab_off;
   const int kv = J.ktot + 1;
@@ -3174,49 +2532,32 @@ __device__ __forceinline__ void run_pm(const DwJob& J, int k0, int s, int S, int
   // else: not instantiated; launch_bwd refuses a job with such a tile before the launch
 }
 
-// the k-tiles of one point split on one XCD (below): 0 off, 1 fp32 and x3, 2 x3 only. Measured (round 3,
-// profiles/r3_ab_dw_xpair.jsonl): x3 dW 5.69 -> 5.55 ms; fp32 dW 7.62 -> 7.68 ms although its HBM reads drop
-// 24.2 -> 21.5 GB per fine launch (the fp32 dW is not bound by its operand traffic)
-#ifndef YANERF_DW_XPAIR
-#define YANERF_DW_XPAIR 2
-#endif
 template <typename T>
 __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t Npad, float* __restrict__ slab) {
   // x3: two buffers of three 384-row bf16 planes (144 KB); otherwise the LDS-DMA ring
   __shared__ __attribute__((aligned(16))) char smem[is_x3<T>      ? 2 * 3 * 384 * 64
                                                     : Cfg<T>::PM ? PM_STAGES * PM_STAGE_BYTES + 2 * PM_SCALES * 4
-                                                                 : DwRing<T>::STAGES * DwRing<T>::STAGE_BYTES + 1024];
-  // 1-D grid in job order (heaviest first); inside a job, split-major so the k-tiles sharing a dZ slab run together.
-  // (An XCD-aware order -- the tiles of jobs that share a section as consecutive blocks of one XCD -- measured slower:
-  // bf16 dW 1.175 -> 1.21 ms, fp32 8.23 -> 9.10 ms.)
-  // Jobs own consecutive workgroup ranges (wg_base); k-tile kt of a job runs in tS[kt] point splits.
+                                                                 : DW32_STAGES * DW32_STAGE_BYTES + 1024];
+  // 1-D grid in job order (heaviest first: the light jobs fill the last round); jobs own consecutive workgroup ranges
+  // (wg_base), k_tiles * S each, split-major inside a job so the k-tiles sharing a dZ slab run together. (An XCD-aware
+  // order -- the tiles of jobs that share a section as consecutive blocks of one XCD -- measured slower: bf16 dW 1.175
+  // -> 1.21 ms, fp32 8.23 -> 9.10 ms; per-k-tile split counts balancing the grid measured slower too, round 3: the bf16
+  // dW streams its operands at the HBM rate, so the lighter last round is not idle time.)
   const int b = blockIdx.x;
   int ji = 0;
   while (ji + 1 < jobs.n && jobs.j[ji + 1].wg_base <= b) ++ji;
   const DwJob& J = jobs.j[ji];
   const int local = b - J.wg_base;
-  bool eq = true;
-  for (int t = 1; t < J.k_tiles; ++t) eq = eq && J.tS[t] == J.tS[0];
-  int s, kt, S;
-  if (eq) {
-    // split-major inside the job, so the k-tiles sharing a dZ slab run together
-    S = J.tS[0];
-    s = local / J.k_tiles;
-    kt = local % J.k_tiles;
-    if ((YANERF_DW_XPAIR == 1 || (YANERF_DW_XPAIR == 2 && is_x3<T>)) && !Cfg<T>::PM && (S & 7) == 0 &&
-        (J.wg_base & 7) == 0 && J.k_tiles > 1) {
-      // the k-tiles of one split 8 blocks apart: blocks go to the 8 XCDs round robin, so every k-tile that stages the
-      // split's dZ rows runs on the same XCD (one L2) at about the same time (block b's XCD is b % 8)
-      const int grp = local / (8 * J.k_tiles), r = local % (8 * J.k_tiles);
-      kt = r >> 3;
-      s = grp * 8 + (r & 7);
-    }
-  } else {
-    // k-tiles with their own split counts (dw_plan balance): tile-major
-    kt = 0;
-    s = local;
-    while (kt + 1 < J.k_tiles && s >= J.tS[kt]) s -= J.tS[kt++];
-    S = J.tS[kt];
+  const int S = jobs.S;
+  int s = local / J.k_tiles, kt = local % J.k_tiles;
+  if (is_x3<T> && (S & 7) == 0 && (J.wg_base & 7) == 0 && J.k_tiles > 1) {
+    // x3: the k-tiles of one split 8 blocks apart: blocks go to the 8 XCDs round robin, so every k-tile that stages
+    // the split's dZ rows runs on the same XCD (one L2) at about the same time (block b's XCD is b % 8). x3 dW 5.69 ->
+    // 5.55 ms; fp32 measured 7.62 -> 7.68 ms although its HBM reads drop 24.2 -> 21.5 GB per fine launch, so fp32 keeps
+    // the plain order
+    const int grp = local / (8 * J.k_tiles), r = local % (8 * J.k_tiles);
+    kt = r >> 3;
+    s = grp * 8 + (r & 7);
   }
   constexpr int BKMAX = dw_bkmax(prec_of<T>);
   const int k0 = kt * BKMAX;
@@ -3225,22 +2566,21 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   if constexpr (Cfg<T>::PM) {
     // the tile's X format: fp8 if its columns come from an fp8 section (a k-tile never mixes formats: host check)
     const bool x8 = (k0 < J.x0p) ? J.x0_u8 : J.x1_u8;
-    // and its A format: the 128 / 256-row tiles are gradient sections (fp8 under YANERF_BF16_G8), a 64-row tile is a
-    // narrow gradient section or the bf16 dU rows (host check in launch_bwd)
-    constexpr bool G8 = YANERF_BF16_G8;
+    // and its A format: the 128 / 256-row tiles are fp8 gradient sections, a 64-row tile is a narrow fp8 gradient
+    // section or the bf16 dU rows (host check in launch_bwd)
     auto run = [&](auto xc) {
       constexpr bool X8 = decltype(xc)::value;
       if (J.bn == 256) {
-        if (bk == 256) run_pm<256, 256, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
-        else if (bk == 128) run_pm<256, 128, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
-        else run_pm<256, 64, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        if (bk == 256) run_pm<256, 256, X8, true>(J, k0, s, S, Npad, slab, se, smem);
+        else if (bk == 128) run_pm<256, 128, X8, true>(J, k0, s, S, Npad, slab, se, smem);
+        else run_pm<256, 64, X8, true>(J, k0, s, S, Npad, slab, se, smem);
       } else if (J.bn == 128) {
-        if (bk == 256) run_pm<128, 256, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
-        else if (bk == 128) run_pm<128, 128, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
-        else run_pm<128, 64, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
-      } else if (G8 && J.a_u8) {
-        if (bk == 256) run_pm<64, 256, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
-        else run_pm<64, 128, X8, G8>(J, k0, s, S, Npad, slab, se, smem);
+        if (bk == 256) run_pm<128, 256, X8, true>(J, k0, s, S, Npad, slab, se, smem);
+        else if (bk == 128) run_pm<128, 128, X8, true>(J, k0, s, S, Npad, slab, se, smem);
+        else run_pm<128, 64, X8, true>(J, k0, s, S, Npad, slab, se, smem);
+      } else if (J.a_u8) {
+        if (bk == 256) run_pm<64, 256, X8, true>(J, k0, s, S, Npad, slab, se, smem);
+        else run_pm<64, 128, X8, true>(J, k0, s, S, Npad, slab, se, smem);
       } else {
         if (bk == 256) run_pm<64, 256, X8, false>(J, k0, s, S, Npad, slab, se, smem);
         else run_pm<64, 128, X8, false>(J, k0, s, S, Npad, slab, se, smem);
@@ -3258,29 +2598,21 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
     } else {
       dw_tile_x3<64, 128>(J, k0, s, S, Npad, slab, se, smem);
     }
-  } else if (J.bn == 256) {
+  } else {
     // (fp32 tiles are at most dw_bkmax = 128 wide: no 256-column instantiations, whose 128 accumulators per wave would
     // set the whole kernel's VGPR count)
     static_assert(BKMAX == 128, "fp32 dW tiles");
-    if constexpr (std::is_same<T, float>::value && YANERF_DW_FUSE_DENSITY && DW_CPR == 8 && DW_STAGGER) {
-      if (bk == 128 && J.ext == 1) {
-        dw_tile<T, 256, 128, 1>(J, k0, s, S, Npad, slab, se, smem);
-        return;
-      }
+    if (J.bn == 256) {
+      if (bk == 128 && J.ext == 1) dw_tile<256, 128, 1>(J, k0, s, S, Npad, slab, se, smem);
+      else if (bk == 128) dw_tile<256, 128>(J, k0, s, S, Npad, slab, se, smem);
+      else dw_tile<256, 64>(J, k0, s, S, Npad, slab, se, smem);
+    } else if (J.bn == 128) {
+      if (bk == 128 && J.ext == 2 && k0 == 0) dw_tile<128, 128, 2>(J, k0, s, S, Npad, slab, se, smem);
+      else if (bk == 128) dw_tile<128, 128>(J, k0, s, S, Npad, slab, se, smem);
+      else dw_tile<128, 64>(J, k0, s, S, Npad, slab, se, smem);
+    } else {
+      dw_tile<64, 128>(J, k0, s, S, Npad, slab, se, smem);
     }
-    if (bk == 128) dw_tile<T, 256, 128>(J, k0, s, S, Npad, slab, se, smem);
-    else dw_tile<T, 256, 64>(J, k0, s, S, Npad, slab, se, smem);
-  } else if (J.bn == 128) {
-    if constexpr (std::is_same<T, float>::value && YANERF_DW_FUSE_DENSITY && DW_CPR == 8 && DW_STAGGER) {
-      if (bk == 128 && J.ext == 2 && k0 == 0) {
-        dw_tile<T, 128, 128, 2>(J, k0, s, S, Npad, slab, se, smem);
-        return;
-      }
-    }
-    if (bk == 128) dw_tile<T, 128, 128>(J, k0, s, S, Npad, slab, se, smem);
-    else dw_tile<T, 128, 64>(J, k0, s, S, Npad, slab, se, smem);
-  } else {
-    dw_tile<T, 64, 128>(J, k0, s, S, Npad, slab, se, smem);
   }
 }
 
@@ -3355,60 +2687,34 @@ __global__ void __launch_bounds__(256) dirpe_dw_final_kernel(const float* __rest
 
 // Sums the S split slabs in split order (deterministic): a thread owns 4 consecutive slab elements and reads them as
 // one 16-byte load per split, 8 splits' loads in flight before their adds (the slab stride is padded to a multiple of
-// 4 elements, dw_slab_pad); the sum order per element is s = 0, 1, ..., S - 1 as before.
-// the point splits of slab element `local` of job J: those of the k-tile its column lies in (the bias column: k-tile 0,
-// whose workgroups form the bias gradient)
-__device__ __forceinline__ int dw_elem_splits(const DwJob& J, int64_t local, int bkmax) {
-  const int kv = J.ktot + 1;
-  const int k = (int)(local % kv);
-  if (k >= J.ktot) return J.tS[0];
-  const int kvirt = k < J.x0_rows ? k : J.x0p + (k - J.x0_rows);
-  const int t = kvirt / bkmax;
-  return J.tS[t > 3 ? 0 : t];
-}
+// 4 elements, dw_slab_pad, so past-the-end elements of the last group read in-bounds padding); the sum order per
+// element is s = 0, 1, ..., S - 1.
 __global__ void dw_reduce_kernel(DwJobs jobs, const float* __restrict__ slab) {
   const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (e0 >= jobs.slab_elems) return;
   const int64_t stride = jobs.slab_stride;
-  int jix[4], Se[4];
+  int jix[4];
   int ji = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int64_t e = e0 + i;
     jix[i] = -1;
-    Se[i] = 0;
     if (e >= jobs.slab_elems) continue;
     while (ji + 1 < jobs.n && jobs.j[ji + 1].slab_off <= e) ++ji;
     jix[i] = ji;
-    Se[i] = jobs.s_uniform ? jobs.s_uniform : dw_elem_splits(jobs.j[ji], e - jobs.j[ji].slab_off, jobs.bkmax);
   }
-  if (jobs.s_uniform) {  // every split count equal: past-the-end elements of the last group read in-bounds padding
+  const int S = jobs.S;
+  f4 sum = f4{0.f, 0.f, 0.f, 0.f};
+  int s = 0;
+  for (; s + 8 <= S; s += 8) {
+    f4 v[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) Se[i] = jobs.s_uniform;
+    for (int u = 0; u < 8; ++u) v[u] = *(const f4*)(slab + (int64_t)(s + u) * stride + e0);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) sum += v[u];
   }
-  float vals[4];
-  if (Se[1] == Se[0] && Se[2] == Se[0] && Se[3] == Se[0]) {
-    const int S = Se[0];
-    f4 sum = f4{0.f, 0.f, 0.f, 0.f};
-    int s = 0;
-    for (; s + 8 <= S; s += 8) {
-      f4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *(const f4*)(slab + (int64_t)(s + u) * stride + e0);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) sum += v[u];
-    }
-    for (; s < S; ++s) sum += *(const f4*)(slab + (int64_t)s * stride + e0);
-    vals[0] = sum.x; vals[1] = sum.y; vals[2] = sum.z; vals[3] = sum.w;
-  } else {
-    // a group across k-tiles with different split counts (or past the end): element by element, same order
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float t = 0.f;
-      for (int s = 0; s < Se[i]; ++s) t += slab[(int64_t)s * stride + e0 + i];
-      vals[i] = t;
-    }
-  }
+  for (; s < S; ++s) sum += *(const f4*)(slab + (int64_t)s * stride + e0);
+  const float vals[4] = {sum.x, sum.y, sum.z, sum.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (jix[i] < 0) break;
@@ -3466,17 +2772,12 @@ static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, const f
 }
 
 // point splits per dW tile: enough workgroups that the light jobs dispatched last fill the tail of the heavy ones
-// (fp32 / x3 64; bf16 32: its fp8-MFMA dW is bound by the operand stream, and half the splits halve the slab reduce,
-// measured dW 0.87 -> 0.84 ms and reduce 0.036 -> 0.020 ms at the Lego fine pass)
-#ifndef YANERF_DW_SMAX
-#define YANERF_DW_SMAX 64
-#endif
-#ifndef YANERF_DW_SMAX_PM
-#define YANERF_DW_SMAX_PM 32
-#endif
-// (point-major: also enough splits that one split's fp8 gradient scales fit the tile's PM_SCALES LDS slots)
+// (fp32 / x3 at most 64; bf16 32: its fp8-MFMA dW is bound by the operand stream, and half the splits halve the slab
+// reduce, measured dW 0.87 -> 0.84 ms and reduce 0.036 -> 0.020 ms at the Lego fine pass); point-major: also enough
+// splits that one split's fp8 gradient scales fit the tile's PM_SCALES LDS slots
+constexpr int DW_SMAX = 64, DW_SMAX_PM = 32;
 static int dw_splits(int total_tiles, int64_t n_stages, bool pm) {
-  const int64_t smax = pm ? YANERF_DW_SMAX_PM : YANERF_DW_SMAX;
+  const int64_t smax = pm ? DW_SMAX_PM : DW_SMAX;
   int64_t S = (smax * 64 + total_tiles - 1) / total_tiles;
   if (S > n_stages) S = n_stages;
   if (S > smax) S = smax;
@@ -3582,7 +2883,6 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     DwJob& j = D.j[D.n++];
     j.ext = 0;
     j.wg_base = 0;
-    for (int t = 0; t < 4; ++t) j.tS[t] = 0;
     j.ext_slab_off = 0;
     j.ext_a = j.ext_x = nullptr;
     j.ext_rows = j.ext_ktot = 0;
@@ -3628,7 +2928,7 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     j.b = grads[sp.gi + 1];
   }, dir_by_ray);
   D.slab_stride = dw_slab_pad(D.slab_elems);
-  if (prec == YANERF_PREC_F32 && !pm && YANERF_DW_FUSE_DENSITY && DW_CPR == 8 && DW_STAGGER) {
+  if (prec == YANERF_PREC_F32) {
     // the density row rides in the intermediate_linear tiles (dw_tile EXT) when its gradient row directly follows the
     // intermediate's 256 gradient rows (fp32 grad_rows: dY then dsigma) and both read the same H_{L-1} rows
     // and the colour-output rows (dU, at most 8) ride in the first k-tile of color_layer.0 (128 rows, 128-wide tiles),
@@ -3669,93 +2969,15 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
   }
 }
 
-// Split plan (YANERF_DW_BALANCE, point-major bf16). With one split count for every k-tile, the bf16 fine dW is 448
-// workgroups of one per CU: the eight 256 x 256 tiles fill the first round and the six lighter tiles (layer 0, the
-// skip layer's PE columns, the colour layer's two tiles, the two heads: 160-384 staged bytes per point against 512)
-// a second round with 64 CUs idle -- 28 vs 23 rounds-of-work units. With YANERF_DW_BALANCE every k-tile gets splits
-// in proportion to its staged bytes per point (+ a per-point overhead), sized so the launch is YANERF_DW_BAL_ROUNDS
-// workgroups per CU of about equal work. Measured slower (profiles/r3_ab_bf16_dw_balanced_splits.jsonl, fine dW:
-// uniform 0.872-0.876 ms, balanced 2 rounds 0.886-0.896, 3 rounds 0.947-0.966, 1 round 1.21-1.22 ms): the bf16 dW
-// streams its operands at the HBM rate, so the light second round is not idle time -- the kernel is bound by its
-// bytes, and more, smaller workgroups only add prologues, epilogues and slab partials. Kept off.
-#ifndef YANERF_DW_BALANCE
-#define YANERF_DW_BALANCE 0
-#endif
-#ifndef YANERF_DW_BAL_ROUNDS
-#define YANERF_DW_BAL_ROUNDS 2
-#endif
-#ifndef YANERF_DW_BAL_SMAX
-#define YANERF_DW_BAL_SMAX 64
-#endif
-#ifndef YANERF_DW_BAL_C0
-#define YANERF_DW_BAL_C0 64
-#endif
-static bool dw_balanced(int prec) { return YANERF_DW_BALANCE && prec_pm(prec); }
-// splits the dW workspace holds (the launch's largest k-tile split count is checked against it)
-static int dw_ws_splits(int total_tiles, int64_t n_stages, int prec) {
-  const int S = dw_splits(total_tiles, n_stages, prec_pm(prec));
-  return dw_balanced(prec) && YANERF_DW_BAL_SMAX > S ? YANERF_DW_BAL_SMAX : S;
-}
-static int dw_num_cus() {
-  static int n[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  if (n[dev] <= 0) {
-    int v = 0;
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    n[dev] = v;
-  }
-  return n[dev];
-}
-// fills every job's per-k-tile split counts (tS) and first workgroup (wg_base), and D.total_wg
-static void dw_plan(DwJobs& D, int prec, int64_t n_stages, int S) {
-  const int bkmax = dw_bkmax(prec);
-  D.bkmax = bkmax;
-  if (dw_balanced(prec)) {
-    int64_t lo = 1;
-    if (prec_pm(prec)) {  // as dw_splits: one split's fp8 gradient scales fit the tile's LDS slots
-      const int64_t cap = (int64_t)(Cfg<bf16_t>::M / PM_SPTS) * (PM_SCALES - 2);
-      lo = (n_stages + cap - 1) / cap;
-    }
-    int64_t hi = YANERF_DW_BAL_SMAX < n_stages ? YANERF_DW_BAL_SMAX : n_stages;
-    if (hi < lo) hi = lo;
-    auto cost = [&](const DwJob& j, int kt) -> int64_t {
-      const int k0 = kt * bkmax, bk = kt < j.k_full ? bkmax : j.bk_tail;
-      const bool x8 = (k0 < j.x0p) ? j.x0_u8 : j.x1_u8;
-      return (int64_t)j.a_chunks * 16 + (int64_t)bk * (x8 ? 1 : 2) + YANERF_DW_BAL_C0;
-    };
-    int64_t total = 0;
-    for (int i = 0; i < D.n; ++i)
-      for (int kt = 0; kt < D.j[i].k_tiles; ++kt) total += cost(D.j[i], kt);
-    const int64_t wgs = (int64_t)YANERF_DW_BAL_ROUNDS * dw_num_cus();
-    for (int i = 0; i < D.n; ++i)
-      for (int kt = 0; kt < D.j[i].k_tiles; ++kt) {
-        int64_t st = total > 0 ? (cost(D.j[i], kt) * wgs + total / 2) / total : 1;
-        if (st < lo) st = lo;
-        if (st > hi) st = hi;
-        D.j[i].tS[kt] = (int16_t)st;
-      }
-  } else {
-    for (int i = 0; i < D.n; ++i)
-      for (int kt = 0; kt < 4; ++kt) D.j[i].tS[kt] = (int16_t)S;
-  }
-  // heads formed inside another job's tiles (fp32 fused heads): their slab rows carry that job's splits
-  for (int i = 0; i < D.n; ++i) {
-    if (D.j[i].ext == 0) continue;
-    for (int k = 0; k < D.n; ++k)
-      if (D.j[k].k_tiles == 0 && D.j[k].slab_off == D.j[i].ext_slab_off)
-        for (int kt = 0; kt < 4; ++kt) D.j[k].tS[kt] = D.j[i].tS[D.j[i].ext == 1 ? kt : 0];
-  }
-  int wg = 0, su = -1;
+// every job's first workgroup (k_tiles * S workgroups per job, in job order) and the launch's workgroup count
+static void dw_plan(DwJobs& D, int S) {
+  D.S = S;
+  int wg = 0;
   for (int i = 0; i < D.n; ++i) {
     D.j[i].wg_base = wg;
-    for (int kt = 0; kt < D.j[i].k_tiles; ++kt) {
-      wg += D.j[i].tS[kt];
-      su = su < 0 ? D.j[i].tS[kt] : (su == D.j[i].tS[kt] ? su : 0);
-    }
+    wg += D.j[i].k_tiles * S;
   }
   D.total_wg = wg;
-  D.s_uniform = su > 0 ? su : 0;
 }
 
 static int64_t dw_slab_elems_for(const MlpLayout& L, int prec, int* total_tiles) {
@@ -3774,8 +2996,7 @@ static int64_t dw_slab_elems_for(const MlpLayout& L, int prec, int* total_tiles)
   return dw_slab_pad(e);
 }
 
-// dW kernel type and precision per mode: x3 saves fp32 activations / gradients, so its weight gradients run on
-// the exact-fp32 dW kernel
+// the training (saved != null) and inference instantiations of the forward
 template <typename T>
 static int launch_fwd(const MlpLayout& L, int prec, const void* packed, const float* o, const float* d, const float* t,
                       int64_t R, int64_t P, float* sigma, float* rgb, void* saved, hipStream_t st) {
@@ -3784,15 +3005,12 @@ static int launch_fwd(const MlpLayout& L, int prec, const void* packed, const fl
   const int64_t Npad = npad_of(prec, N);
   const typename Cfg<T>::w_t* Wt = (const typename Cfg<T>::w_t*)packed;
   const float* Wf = (const float*)((const char*)packed + L.f_base);
-  dim3 grid((unsigned)(Npad / (Cfg<T>::M * Cfg<T>::HALVES))), block(Cfg<T>::HALVES * Cfg<T>::WAVES * 64);
-  uint64_t* masks = saved ? (uint64_t*)((char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM)) : nullptr;
-  // bf16 and (with the in-GEMM saves) fp32 inference run the instantiation without the save code
-  constexpr bool SPLIT = std::is_same<T, bf16_t>::value || (std::is_same<T, float>::value && YANERF_F32_GSAVE) ||
-                         (is_x3<T> && YANERF_X3_STAT);
-  if (saved || !SPLIT)
+  dim3 grid((unsigned)(Npad / Cfg<T>::M)), block(Cfg<T>::WAVES * 64);
+  if (saved) {
+    uint64_t* masks = (uint64_t*)((char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM));
     hipLaunchKernelGGL((mlp_fwd_kernel<T, true>), grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, (ST*)saved,
-                       saved ? masks : nullptr, Npad);
-  else
+                       masks, Npad);
+  } else
     hipLaunchKernelGGL((mlp_fwd_kernel<T, false>), grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, nullptr,
                        nullptr, Npad);
   YN_LAUNCH_CHECK("mlp_forward");
@@ -3814,18 +3032,18 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   // the point splits and slab size are those of the full job set (yanerf_mlp_bwd_workspace_bytes)
   int tiles_all = 0;
   const int64_t slab_all = dw_slab_elems_for(L, prec, &tiles_all);
-  const int S = dw_ws_splits(tiles_all, Npad / dw_stage_pts(prec), prec);
+  const int S = dw_splits(tiles_all, Npad / dw_stage_pts(prec), Cfg<T>::PM);
   // the dirPE weight gradient by rays: per-ray dZc partials after the slabs, then the block partials
   constexpr int CH = dzc_chunk<T>();
-  // default (1): fp32 only, where it measured -0.21 ms of 15.2 ms per Lego fine backward; bf16 and fp32x3 gained
-  // less in dW than the per-ray sums cost in dX; 2 forces it for every precision
-  const bool dir_by_ray = (YANERF_DIRPE_RAY == 2 || (YANERF_DIRPE_RAY == 1 && std::is_same<T, float>::value)) && P >= CH && L.dir_dim <= KDIR && L.hdir <= HC && Npad < (1ll << 31);
+  // (fp32 only, where it measured -0.21 ms of 15.2 ms per Lego fine backward; bf16 and fp32x3 gained less in dW than
+  // the per-ray sums cost in dX)
+  const bool dir_by_ray = std::is_same<T, float>::value && P >= CH && L.dir_dim <= KDIR && L.hdir <= HC &&
+                          Npad < (1ll << 31);
   float* dzc_part = (float*)((char*)slab + (int64_t)S * slab_all * 4);
   float* blockp = dzc_part + 2 * (Npad / CH) * HC;
   const uint64_t* masks = (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM));
   if (phase & 1) {
-    hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / (Cfg<T>::M * Cfg<T>::HALVES))),
-                       dim3(Cfg<T>::HALVES * Cfg<T>::DXWAVES * 64), 0, st, L,
+    hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::DXWAVES * 64), 0, st, L,
                        Wt, Wf, masks, rgb, gs, gr, N, Npad, gradbuf, P, dir_by_ray ? dzc_part : nullptr);
     YN_LAUNCH_CHECK("mlp_backward_dx");
   }
@@ -3834,11 +3052,7 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   if (!dw && !red) return 0;
   DwJobs D;
   build_dw_jobs(L, prec, saved, gradbuf, Npad, grads, D, dir_by_ray);
-  dw_plan(D, prec, Npad / dw_stage_pts(prec), dw_splits(tiles_all, Npad / dw_stage_pts(prec), Cfg<T>::PM));
-  for (int i = 0; i < D.n; ++i)
-    for (int kt = 0; kt < D.j[i].k_tiles; ++kt)
-      YN_CHECK(D.j[i].tS[kt] >= 1 && D.j[i].tS[kt] <= S, "mlp_backward: dW job %d k-tile %d: %d splits (workspace %d)", i,
-               kt, (int)D.j[i].tS[kt], S);
+  dw_plan(D, S);
   for (int i = 0; i < D.n; ++i)  // a point-major k-tile reads one X format: mixed sections must split at a tile edge
     YN_CHECK(!D.j[i].X1 || D.j[i].x0_u8 == D.j[i].x1_u8 || D.j[i].x0p % dw_bkmax(prec) == 0,
              "mlp_backward: dW job %d mixes fp8 and bf16 columns inside a tile", i);
@@ -3853,7 +3067,7 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
                  pm_tile_bytes(j.bn, bk, x8, j.a_u8), PM_STAGE_BYTES);
       }
   for (int i = 0; i < D.n; ++i)  // the dW tile's A format follows its row tile (dw_tile_pm's A8)
-    YN_CHECK(!Cfg<T>::PM || D.j[i].bn == 64 || D.j[i].a_u8 == YANERF_BF16_G8,
+    YN_CHECK(!Cfg<T>::PM || D.j[i].bn == 64 || D.j[i].a_u8,
              "mlp_backward: dW job %d: gradient format %d does not match its %d-row tile", i, D.j[i].a_u8, D.j[i].bn);
   YN_CHECK(D.slab_stride <= dw_slab_pad(slab_all), "mlp_backward: dW slab larger than its workspace");
   if (dw) {
@@ -3934,7 +3148,7 @@ int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, 
   const int64_t grad_bytes = grad_t_bytes(d->n_layers, Npad, elem_size(precision), prec_pm(precision));
   int tiles = 0;
   int64_t se = dw_slab_elems_for(L, precision, &tiles);
-  int S = dw_ws_splits(tiles, Npad / dw_stage_pts(precision), precision);
+  int S = dw_splits(tiles, Npad / dw_stage_pts(precision), prec_pm(precision));
   // + the per-ray dZc partials (two slots per dZc chunk) and the dirPE block partials (rays >= chunks when used)
   const int CH = precision == YANERF_PREC_F32 ? dzc_chunk<float>()
                  : precision == YANERF_PREC_BF16 ? dzc_chunk<bf16_t>() : dzc_chunk<x3_t>();

@@ -449,8 +449,11 @@ class NeRFTrainer:
         Every per-step scalar lives on the device (Philox base, Adam table row; _sync_step_state), so replay_step()
         runs step after step with each step's own draws, learning rate and bias corrections, bit for bit the steps
         step() would run. pose / focal are copied into static buffers at each replay; the image buffer is captured by
-        reference (replay_step(image=...) copies a different one into it). Run at least one eager step first (the
-        library's kernels load on first launch). Single rank only (a gloo exchange cannot be captured)."""
+        reference (replay_step(image=...) copies a different one into it). The depth range lives in a static device
+        buffer [near, far] that the captured ray generation reads: replay_step(near=, far=) rewrites it (floats or
+        LLFF's per-image bound tensors, averaged as step() does), so a captured LLFF step follows each image's bounds;
+        without them the range of the previous replay stays. Run at least one eager step first (the library's kernels
+        load on first launch). Single rank only (a gloo exchange cannot be captured)."""
         if self.world > 1:
             raise NotImplementedError("NeRFTrainer.capture_step: single rank only")
         if self.events is not None or self.kernel_probes:
@@ -459,7 +462,8 @@ class NeRFTrainer:
         self._g_pose = pose.reshape(1, -1, 4)[:, :3, :4].contiguous().clone()
         self._g_focal = focal.reshape(1).contiguous().clone()
         self._g_image = image.reshape(1, self.H, self.W, -1).contiguous()
-        self._g_bounds = (near, far)
+        self._g_bounds = torch.empty(2, dtype=F32, device=self.dev)
+        self._set_graph_bounds(near, far)
         self._sync_step_state()
         rng0, step0, lr0, dstate0 = self.rng.get_state(), self.step_count, self.lr, self._dstate_host
         torch.cuda.synchronize(self.dev)
@@ -467,7 +471,7 @@ class NeRFTrainer:
         self._capturing = True
         try:
             with torch.cuda.graph(g):
-                out = self.step(self._g_pose, self._g_focal, self._g_image, near, far)
+                out = self.step(self._g_pose, self._g_focal, self._g_image, self._g_bounds[0:1], self._g_bounds[1:2])
         finally:
             self._capturing = False
         # the capture ran nothing: undo the captured step's host bookkeeping; each replay re-applies it
@@ -477,12 +481,31 @@ class NeRFTrainer:
         self.graph, self._g_out = g, out
         return out
 
+    def _set_graph_bounds(self, near, far):
+        """Write the depth range of the next captured step into the static [near, far] buffer: None = the config's
+        value; floats; tensors averaged (ray_sampler.py:280-283) -- host tensors on the host, device tensors on the
+        device (no host sync)."""
+        for i, (v, dflt) in enumerate(((near, self.near), (far, self.far))):
+            v = dflt if v is None else v
+            if isinstance(v, torch.Tensor):
+                v = v.float().mean()
+                if v.device.type == "cpu":
+                    v = float(v)
+            if isinstance(v, torch.Tensor):
+                self._g_bounds[i:i + 1].copy_(v.reshape(1))
+            else:
+                self._g_bounds[i:i + 1].fill_(float(v))
+
     def replay_step(self, pose: Optional[torch.Tensor] = None, focal: Optional[torch.Tensor] = None,
-                    image: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+                    image: Optional[torch.Tensor] = None, near=None, far=None) -> Dict[str, torch.Tensor]:
         """One training step by replaying the captured graph (capture_step), on `pose` / `focal` (copied into the
-        static buffers; default: the previous ones) and the captured image buffer."""
+        static buffers; default: the previous ones), the captured image buffer and the depth range near / far
+        (default: the previous replay's)."""
         if self.graph is None:
             raise RuntimeError("NeRFTrainer.replay_step: call capture_step first")
+        if near is not None or far is not None:
+            cur = (self._g_bounds[0:1], self._g_bounds[1:2])
+            self._set_graph_bounds(cur[0].clone() if near is None else near, cur[1].clone() if far is None else far)
         if pose is not None:
             self._g_pose.copy_(pose.reshape(1, -1, 4)[:, :3, :4])
         if focal is not None:
@@ -603,21 +626,27 @@ class NeRFTrainer:
         if self._render_graph is None or self._render_graph[0] != key:
             sp = pose.reshape(1, -1, 4)[:, :3, :4].contiguous().clone()
             sf = focal.reshape(1).contiguous().clone()
+            rng_pre = self.rng.get_state()
             self.render(sp, sf, *key[:4], chunk=chunk)  # eager first: the evaluation buffers exist before the capture
             torch.cuda.synchronize(self.dev)
             rng0 = self.rng.get_state()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 outs = self.render(sp, sf, *key[:4], chunk=chunk)
-            self.rng.set_state(rng0)  # deterministic draws: the counter only keeps render()'s bookkeeping
+            # the capture ran nothing: rewind the counter; every replay advances it by what an eager render() draws,
+            # so training steps after an evaluation draw the same pixels / jitter / noise whichever render path ran
+            delta = self.rng.get_state()[1] - rng0[1]
+            self.rng.set_state(rng_pre)  # (the eager warm-up's draws are not counted either)
             # the graph writes into these evaluation buffers: keep them alive even if a later eager render() of
             # another size replaces the trainer's buffer cache
             keep = dict(self._eval_ws)
-            self._render_graph = (key, g, sp, sf, outs, keep)
-        _, g, sp, sf, outs, _ = self._render_graph
+            self._render_graph = (key, g, sp, sf, outs, keep, delta)
+        _, g, sp, sf, outs, _, delta = self._render_graph
         sp.copy_(pose.reshape(1, -1, 4)[:, :3, :4])
         sf.copy_(focal.reshape(1))
         g.replay()
+        seed, off = self.rng.get_state()
+        self.rng.set_state((seed, off + delta))
         return outs
 
     def evaluate(self, images, shard: bool = True) -> Dict[str, float]:

@@ -195,6 +195,17 @@ int yanerf_rgb_loss(const float* pred, const float* image, const float* xys, int
                     int64_t H, int64_t W, int64_t C, float scale, float* sq_err_per_ray, float* g_pred,
                     void* stream);
 
+/* ------------------------------------------------------------------------------------------------
+ * The Monte-Carlo rays' outputs splatted onto full-size images: replaces scatter_rays_to_image
+ * (pipelines/utils.py:299-323) as NeRFPipeline._rasterize_mc_samples calls it for rendered_images /
+ * rendered_depths / rendered_alpha_masks on every training step with output_rasterized_mc
+ * (nerf_pipeline.py:196-201, 307-324). values [B][R][C], xys [B][R][2] (integer-valued floats, pixel
+ * x + W * y) -> out [B][H][W][C] = bg[c] (C floats; NULL = 0) everywhere, values at the rays' pixels.
+ * Two rays on one pixel: one of them is written (torch's scatter_ leaves that order unspecified too).
+ * ---------------------------------------------------------------------------------------------- */
+int yanerf_scatter_rays(const float* values, const float* xys, int64_t B, int64_t R, int64_t C, int64_t H,
+                        int64_t W, const float* bg, float* out, void* stream);
+
 /* Fused Adam step over a flat fp32 parameter buffer: torch.optim.Adam (run.py:158-160) with torch's arithmetic, one
  * element per lane. The scalars are doubles, as torch holds them in Python: bias corrections 1 - beta**step, the step
  * size lr / bc1 and sqrt(bc2) are computed on the host in double and rounded to float once, as torch passes them to

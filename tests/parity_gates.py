@@ -56,10 +56,21 @@ def oracle_fine_at(O, params_f, arch, origins, directions, raymarch_opts, bg=(0.
     return fine_at
 
 
+def reference_sensitive_rays(sens, z_tol=2e-5):
+    """The rays the REFERENCE itself moves by more than z_tol under equally valid fp32 evaluations of its coarse stage
+    (tests/golden/sensitivity_*.npz, make_golden.gen_sensitivity: float64 end to end, exp one ulp off, coarse
+    parameters one ulp off, Linear K-sums reordered): a boolean mask over the rays."""
+    f64 = np.abs(np.asarray(sens["z_fine_f64"], np.float64) - sens["z_fine"]).max(-1) > z_tol
+    return (np.asarray(sens["max_z_move"]) > z_tol) | f64
+
+
 def split_gate(rgb, rgb_ref, z, z_ref, depth=None, depth_ref=None, *, fine_at=None, coarse=None, strict=1e-5,
-               strict_depth=1e-4, z_tol=2e-5, tag=""):
+               strict_depth=1e-4, z_tol=2e-5, tag="", sensitivity=None):
     """coarse = (O, lengths [R,Pc], our coarse weights [R,Pc], n_fine): the oracle refinement of our coarse weights
-    (deterministic, as the evaluation pass runs it) must equal z on every ray."""
+    (deterministic, as the evaluation pass runs it) must equal z on every ray.
+    sensitivity = the reference's own sensitivity golden of this render (reference_sensitive_rays): the number of rays
+    whose refined depths differ between this build and the reference must not exceed the number the reference itself
+    moves under ulp-level changes of its coarse stage; the rays outside that set are counted in the report."""
     R = len(z)
     rgb = np.asarray(rgb, np.float64).reshape(R, -1)
     rgb_ref = np.asarray(rgb_ref, np.float64).reshape(R, -1)
@@ -75,6 +86,13 @@ def split_gate(rgb, rgb_ref, z, z_ref, depth=None, depth_ref=None, *, fine_at=No
         depth = np.asarray(depth, np.float64).reshape(-1)
         derr = np.abs(depth - np.asarray(depth_ref, np.float64).reshape(-1))
         report["max_depth_err_same_depths"] = float(derr[same].max()) if same.any() else 0.0
+    if sensitivity is not None:
+        sens = reference_sensitive_rays(sensitivity, z_tol)
+        assert sens.shape == same.shape, (sens.shape, same.shape)
+        report.update(reference_sensitive_rays=int(sens.sum()),
+                      reference_moved_by_f64=int((np.abs(np.asarray(sensitivity["z_fine_f64"]) - sensitivity["z_fine"])
+                                                  .max(-1) > z_tol).sum()),
+                      rays_with_other_depths_outside_reference_sensitive=int((~same & ~sens).sum()))
     if coarse is not None:
         O, zc, w_ours, n_fine = coarse
         zc = np.asarray(zc, np.float32).reshape(R, -1)
@@ -94,6 +112,8 @@ def split_gate(rgb, rgb_ref, z, z_ref, depth=None, depth_ref=None, *, fine_at=No
         assert report["max_depth_err_same_depths"] <= strict_depth, report
     if coarse is not None:
         assert report["max_depth_err_vs_oracle_refine_of_our_weights"] <= z_tol, report
+    if sensitivity is not None:
+        assert report["rays_with_other_depths"] <= report["reference_sensitive_rays"], report
     if flip.size:
         assert fine_at is not None, f"{flip.size} rays with other refined depths and no fine_at to account for them"
         assert coarse is not None, f"{flip.size} rays with other refined depths: pass `coarse` to close the loop"
@@ -109,15 +129,75 @@ def grad_err(v, ref) -> float:
     return float(np.abs(v - ref).max() / max(np.abs(ref).max(), 1e-30))
 
 
-def loose_grad_gate(v, ref, name):
-    """The end-to-end gate for gradients that sum over rays whose refined depths may have flipped (split_gate):
-    >= 98 % of elements within 5e-3 * max, all within 3e-2 * max. Returns the relative L2 error."""
+def loose_grad_gate(v, ref, name, enforce: bool = True):
+    """The end-to-end statistical view of gradients that sum over rays whose refined depths may have flipped
+    (split_gate): >= 98 % of elements within 5e-3 * max, all within 3e-2 * max. Returns the relative L2 error. The
+    parity tests report it (enforce=False) beside the strict per-element tie-budget gate below."""
     v, ref = np.asarray(v, np.float64), np.asarray(ref, np.float64)
     mx = np.abs(ref).max()
     err = np.abs(v - ref)
-    assert err.max() <= 3e-2 * mx, (name, err.max() / mx)
-    assert (err <= 5e-3 * mx).mean() >= 0.98, (name, (err <= 5e-3 * mx).mean())
+    if enforce:
+        assert err.max() <= 3e-2 * mx, (name, err.max() / mx)
+        assert (err <= 5e-3 * mx).mean() >= 0.98, (name, (err <= 5e-3 * mx).mean())
     return float(np.linalg.norm(v - ref) / max(np.linalg.norm(ref), 1e-30))
+
+
+# the oracle's gradients under the reference's own ReLU decisions and refined depths against the reference's
+# (test_oracle_golden.test_train_step_lego_strict_under_reference_relu_decisions: measured 7.5e-6 coarse, 1.6e-5 fine)
+ORACLE_PIN = 2e-5
+
+
+def golden_grad_items(g, models):
+    """(model index, name, ours, reference, index into the flattened tensor or None) for every parameter gradient the
+    train-step golden holds: whole tensors up to 4,096 elements, a fixed sample of 256 entries of the larger ones."""
+    for i, m in enumerate(models):
+        for name, p in m.named_parameters():
+            v = p.grad.detach().float().cpu().numpy().astype(np.float64).reshape(-1)
+            if f"grad{i}:{name}" in g:
+                yield i, name, v, g[f"grad{i}:{name}"].astype(np.float64).reshape(-1), None
+            else:
+                idx = g[f"gradidx{i}:{name}"]
+                yield i, name, v[idx], g[f"gradval{i}:{name}"].astype(np.float64), idx
+
+
+def tie_budget_gate(v, ref, o_hip, o_ref, name, strict: float = STRICT_GRAD, pin: float = ORACLE_PIN) -> dict:
+    """The direct comparison with the reference's gradient, strict per element with the ReLU ties (and, for a fine pass
+    at this build's own refined depths, the sample_pdf flips) as an explicit budget:
+
+        |ours - reference| <= strict * max|reference| + |O_hip - O_ref|     (every element)
+
+    O_hip = the reference's algorithm (oracle) under the ReLU decisions this build took (at its refined depths),
+    O_ref = the same under the reference's own recorded decisions (at the reference's depths), itself pinned to the
+    reference (|O_ref - reference| <= pin * max, asserted here). |O_hip - O_ref| is exactly what the differing decisions
+    (fp32 ties at the kink, flipped samples) contribute; whatever ours differs by beyond it must be within `strict`.
+    Returns {direct, budget, residual, pin}: max |ours - ref|, max |O_hip - O_ref|, max (|ours - ref| - |O_hip - O_ref|)
+    and max |O_ref - ref|, each relative to max |ref|."""
+    v, ref, o_hip, o_ref = (np.asarray(x, np.float64).reshape(-1) for x in (v, ref, o_hip, o_ref))
+    M = max(np.abs(ref).max(), 1e-30)
+    pin_err = float(np.abs(o_ref - ref).max() / M)
+    assert pin_err <= pin, (name, "oracle under the reference's decisions vs the reference", pin_err)
+    budget = np.abs(o_hip - o_ref)
+    direct = np.abs(v - ref)
+    excess = direct - budget
+    rep = dict(direct=float(direct.max() / M), budget=float(budget.max() / M),
+               residual=float(max(excess.max(), 0.0) / M), pin=pin_err)
+    assert excess.max() <= strict * M, (name, rep)
+    return rep
+
+
+def summarize_tie_budget(per_tensor: dict) -> dict:
+    """Per model: the worst direct error, tie budget and residual over its tensors (for the parity report)."""
+    out = {}
+    for i in sorted({k[0] for k in per_tensor}):
+        rows = [r for k, r in per_tensor.items() if k[0] == i]
+        tag = "coarse" if i == 0 else "fine"
+        out[f"{tag}_direct_max"] = max(r["direct"] for r in rows)
+        out[f"{tag}_tie_budget_max"] = max(r["budget"] for r in rows)
+        out[f"{tag}_residual_max"] = max(r["residual"] for r in rows)
+        out[f"{tag}_oracle_pin_max"] = max(r["pin"] for r in rows)
+    out["per_tensor"] = {f"{k[0]}:{k[1]}": {kk: float(f"{vv:.3e}") for kk, vv in r.items()}
+                         for k, r in per_tensor.items()}
+    return out
 
 
 def golden_grad_pairs(g, models):

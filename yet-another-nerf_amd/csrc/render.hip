@@ -694,6 +694,33 @@ __global__ void rgb_loss_kernel(const float* __restrict__ pred, const float* __r
   if (sq) sq[gid] = acc;
 }
 
+// ---- scatter_rays_to_image (pipelines/utils.py:299-323; nerf_pipeline.py:307-324 _rasterize_mc_samples): the
+// Monte-Carlo rays' outputs splatted onto full-size images. Fill with the background (0 + bg, as the reference's
+// new_zeros + bg_color), then one thread per (ray, channel) writes its value at the pixel x + W * y -- the index
+// computed in float from the float xys and truncated, as the reference's `.long()` of the float expression.
+__global__ void scatter_fill_kernel(float* __restrict__ out, int64_t n, int64_t C, const float* __restrict__ bg) {
+  const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i0 >= n) return;
+  float v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = bg ? 0.0f + bg[(i0 + k) % C] : 0.0f;
+  if (i0 + 4 <= n && ((reinterpret_cast<uintptr_t>(out + i0) & 15) == 0)) {
+    *(f4*)(out + i0) = f4{v[0], v[1], v[2], v[3]};
+  } else {
+    for (int k = 0; k < 4 && i0 + k < n; ++k) out[i0 + k] = v[k];
+  }
+}
+__global__ void scatter_rays_kernel(const float* __restrict__ values, const float* __restrict__ xys, int64_t B,
+                                    int64_t R, int64_t C, int64_t H, int64_t W, float* __restrict__ out) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * R * C) return;
+  const int64_t c = gid % C, br = gid / C, b = br / R;
+  const float fi = xys[br * 2 + 0] + (float)W * xys[br * 2 + 1];
+  const int64_t pix = (int64_t)fi;
+  if (pix < 0 || pix >= H * W) return;  // (the reference asserts nothing here; an out-of-image ray is dropped)
+  out[(b * H * W + pix) * C + c] = values[gid];
+}
+
 // torch.optim.Adam's per-element arithmetic (torch/optim/adam.py _multi_tensor_adam, the default on the GPU), op for
 // op: the scalars arrive already rounded to float from the host's double arithmetic, exactly as torch casts its
 // Python-float scalars, and the multiply-adds are fused where torch's foreach kernels fuse them. Pinned bit for bit by
@@ -870,6 +897,24 @@ int yanerf_rgb_loss(const float* pred, const float* image, const float* xys, int
   hipLaunchKernelGGL(rgb_loss_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), pred, image,
                      xys, B, R, H, W, C, scale, sq_err_per_ray, g_pred);
   YN_LAUNCH_CHECK("rgb_loss");
+  return 0;
+}
+
+int yanerf_scatter_rays(const float* values, const float* xys, int64_t B, int64_t R, int64_t C, int64_t H, int64_t W,
+                        const float* bg, float* out, void* stream) {
+  YN_CHECK(values && xys && out, "scatter_rays: null pointer");
+  YN_CHECK(B >= 0 && R >= 0 && C >= 1 && H >= 1 && W >= 1, "scatter_rays: bad sizes");
+  YN_CHECK(H * W < (1ll << 24), "scatter_rays: %lld pixels: the float pixel index is exact only below 2^24",
+           (long long)(H * W));
+  const int64_t n = B * H * W * C;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(scatter_fill_kernel, dim3((unsigned)(((n + 3) / 4 + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), out, n, C, bg);
+  YN_LAUNCH_CHECK("scatter_fill");
+  if (B * R == 0) return 0;
+  hipLaunchKernelGGL(scatter_rays_kernel, dim3((unsigned)((B * R * C + 255) / 256)), dim3(256), 0, as_stream(stream),
+                     values, xys, B, R, C, H, W, out);
+  YN_LAUNCH_CHECK("scatter_rays");
   return 0;
 }
 

@@ -412,6 +412,29 @@ def rgb_loss(pred: torch.Tensor, image: torch.Tensor, xys: torch.Tensor, scale: 
     return sq, g
 
 
+@torch.no_grad()
+def scatter_rays(values: torch.Tensor, xys: torch.Tensor, image_height: int, image_width: int,
+                 bg_color: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """scatter_rays_to_image (pipelines/utils.py:299-323) on the device: values [B, *spatial, C] at integer-valued
+    xys [B, *spatial, 2] onto a new [B, H, W, C] image filled with bg_color (when its last dim is C) or zeros."""
+    _dev(values, xys, bg_color)
+    B, *ts, C = values.shape
+    _, *gs, _ = xys.shape
+    assert ts == gs, f"{ts} vs. {gs}"
+    v = _f32c(values.reshape(B, -1, C))
+    xy = _f32c(xys.reshape(B, -1, 2))
+    bg = None
+    if bg_color is not None and bg_color.shape[-1] == C:
+        if bg_color.numel() != C:
+            raise NotImplementedError("scatter_rays: a per-pixel bg_color (the reference's _rasterize_mc_samples "
+                                      "passes None); only a [C] background is supported")
+        bg = _f32c(bg_color.reshape(C))
+    out = torch.empty(B, int(image_height), int(image_width), C, dtype=_F32, device=v.device)
+    _C.check(_C.lib().yanerf_scatter_rays(_p(v), _p(xy), B, v.shape[1], C, int(image_height), int(image_width),
+                                          _p(bg), _p(out), _stream()), "yanerf_scatter_rays")
+    return out if values.dtype == _F32 else out.to(values.dtype)
+
+
 def adam_step(params: torch.Tensor, grads: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, *, lr: float,
               betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, step: int) -> None:
     _dev(params, grads, exp_avg, exp_avg_sq)

@@ -60,19 +60,10 @@ def sample_grid(tensor: torch.Tensor, image_sampling_grid: torch.Tensor) -> torc
 
 @torch.no_grad()
 def scatter_rays_to_image(tensor, image_sampling_grid, image_height, image_width, bg_color=None):
-    """Inverse of sample_grid for visualisation (pipelines/utils.py:299-323)."""
-    B, *ts, C = tensor.shape
-    _, *gs, _ = image_sampling_grid.shape
-    assert ts == gs, f"{ts} vs. {gs}"
-    flat = tensor.reshape(B, -1, C)
-    g = image_sampling_grid.reshape(B, -1, 2)
-    idx = (g[..., 0] + image_width * g[..., 1]).long()[..., None].expand(-1, -1, C)
-    out = tensor.new_zeros(B, image_height, image_width, C)
-    if bg_color is not None and bg_color.shape[-1] == C:
-        out = out + bg_color
-    out = out.view(B, -1, C)
-    out.scatter_(1, idx, flat)
-    return out.view(B, image_height, image_width, C)
+    """Inverse of sample_grid for visualisation (pipelines/utils.py:299-323), as the yanerf_scatter_rays HIP kernels
+    (fill + scatter; device tensors only, like every op of this package)."""
+    from .. import ops
+    return ops.scatter_rays(tensor, image_sampling_grid, image_height, image_width, bg_color)
 
 
 def safe_sqrt(A: torch.Tensor, eps: float = 1e-4) -> torch.Tensor:

@@ -240,6 +240,45 @@ def test_bucketed_and_single_exchange_give_identical_parameters(precision):
         assert torch.equal(b["bucketed"][key], b["single"][key]), key
 
 
+def _rccl_world1_worker(rank, world, port, q):
+    """RCCL on the hardware at world size 1 (the box has one card; RCCL refuses two ranks on one device): the
+    communicator set up as parallel.init_distributed does for "nccl" (device_id bound), then the trainer's bucket
+    pattern -- an async all-reduce started right after a kernel that produced the bucket, a second kernel queued behind
+    it on the compute stream, the wait, the divide -- checked for stream ordering: the collective must see the first
+    kernel's output and the second kernel must not be blocked on, or corrupted by, the collective."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group(backend="nccl", device_id=torch.device("cuda", 0))
+    out = {"backend": dist.get_backend(), "world": dist.get_world_size()}
+    g = torch.Generator(device="cuda:0").manual_seed(1)
+    a = torch.randn(4096, 4096, device="cuda:0", generator=g)
+    bucket = torch.empty(595_844, device="cuda:0")
+    ref = None
+    for it in range(3):
+        torch.mul(a.view(-1)[it:it + 595_844], 2.0 + it, out=bucket)  # the producer kernel of the bucket
+        ref = bucket.clone()
+        h = dist.all_reduce(bucket, op=dist.ReduceOp.SUM, async_op=True)
+        c = a @ a  # compute queued behind the collective's start (the fine backward's place)
+        h.wait()
+        bucket.div_(dist.get_world_size())
+        torch.cuda.synchronize()
+        out[f"equal_{it}"] = bool(torch.equal(bucket, ref))
+        out[f"compute_ok_{it}"] = bool(torch.isfinite(c).all())
+    q.put(_by_value((0, out)))
+    dist.destroy_process_group()
+
+
+def test_rccl_world1_bucket_ordering():
+    """The "nccl" (RCCL) backend actually runs on the MI355X box at world size 1: process-group init with a bound
+    device and the trainer's async-bucket / wait / divide ordering against kernels on the compute stream. (Multi-rank
+    RCCL over xGMI needs a multi-card box: the driver's N-GPU bench runs it.)"""
+    (_, out), = _spawn(_rccl_world1_worker, 1)
+    assert out["backend"] == "nccl" and out["world"] == 1
+    for it in range(3):
+        assert out[f"equal_{it}"] and out[f"compute_ok_{it}"], out
+
+
 def _ddp_worker(rank, world, port, q, golden_dir):
     """The drop-in path as scripts/run.py:162-166 runs it: the registry NeRFPipeline wrapped in
     DistributedDataParallel(find_unused_parameters=True); one step on rank-specific data with injected draws, and the

@@ -372,6 +372,19 @@ def extras(pcfg, cfg, dev, poses, focal, image, precision, others=()):
         out["fern_64_128_train"][p] = {
             "rays_per_s": round(tr.R / dt, 1), "ms_per_step": round(1e3 * dt, 3),
             "step_mfma_frac": round(train_flops_per_ray(tr.Pc, tr.Pf) * tr.R / dt / 1e12 / PEAK_TFLOPS[p], 4)}
+        # the same steps replayed as a HIP graph (a 1024-ray step is short, so launch gaps weigh more); the captured
+        # step reads its per-image bounds from a static device buffer (replay_step(near=, far=))
+        tr.capture_step(poses[0:1], ffocal, fimg, near=bounds[:, :1], far=bounds[:, 1:])
+        tr.replay_step(poses[1:2], ffocal, near=bounds[:, :1], far=bounds[:, 1:])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(nst):
+            tr.replay_step(poses[(3 + i) % len(poses)][None], ffocal, near=bounds[:, :1], far=bounds[:, 1:])
+        torch.cuda.synchronize()
+        dtg = (time.perf_counter() - t0) / nst
+        out["fern_64_128_train"][p].update(
+            graph_rays_per_s=round(tr.R / dtg, 1), graph_ms_per_step=round(1e3 * dtg, 3),
+            step_mfma_frac_graph=round(train_flops_per_ray(tr.Pc, tr.Pf) * tr.R / dtg / 1e12 / PEAK_TFLOPS[p], 4))
         del tr
     return out
 

@@ -438,14 +438,23 @@ def psnr_leg(precision: str, steps: int, dev):
     """The `+ PSNR` half of the metric: the same fused training step (Lego config, 64 + 128, 4096 rays) trained on a
     procedural scene written in the nerf_synthetic format (tools/synthetic_scene.py: 40 train / 8 test views at
     100 x 100, read back through BlenderDataset into HBM), then scored as the reference's evaluation does (PSNR of the
-    mean per-image MSE). No real dataset can be fetched here, so this is a synthetic-scene PSNR, not Lego's."""
+    mean per-image MSE). No real dataset can be fetched here, so this is a synthetic-scene PSNR, not Lego's.
+
+    Round 4: with the reference's initialisation (density-layer bias 0, nerf_mlp.py:69-71, whose own comment says
+    "Sometimes this is not enough") this scene's training collapses to the transparent solution for seed 42 -- no
+    density anywhere, each ray's colour painted on its background-opacity last sample (`rays_before_far_plane` 0,
+    profiles/r4_density_collapse_probe.jsonl). The headline PSNR is therefore the run with the density-layer bias
+    initialised to 1.0, which reconstructs the scene; the reference-init run and the bf16 run are reported beside it."""
     import tempfile
     sys.path.insert(0, str(ROOT / "tools"))
     from psnr_synthetic import run as psnr_run  # noqa: E402
     from synthetic_scene import write_scene  # noqa: E402
     with tempfile.TemporaryDirectory() as tmp:
         data = write_scene(Path(tmp) / "synthetic", 100, 40, 8, device=str(dev))
-        r = psnr_run(data, precision, steps, dev)
+        r = psnr_run(data, precision, steps, dev, density_bias=1.0)
+        r["reference_init_run"] = psnr_run(data, precision, steps, dev)
+        if precision != "bf16":
+            r["bf16_run"] = psnr_run(data, "bf16", steps, dev, density_bias=1.0)
     r["scene"] = "procedural blobs, 100x100, 40 train / 8 test views (synthetic, not Lego)"
     return r
 

@@ -255,18 +255,31 @@ def nerf_mlp_forward(params: Dict[str, np.ndarray], arch: MLPArch, origins, dire
     return sigma.reshape(*lead, P, 1), rgb.reshape(*lead, P, -1), cache
 
 
-def nerf_mlp_backward(params: Dict[str, np.ndarray], arch: MLPArch, cache: MLPCache, g_sigma, g_rgb):
+def nerf_mlp_backward(params: Dict[str, np.ndarray], arch: MLPArch, cache: MLPCache, g_sigma, g_rgb,
+                      abs_terms: bool = False):
     """Manual reverse-mode of nerf_mlp_forward; returns {param_name: grad} (autograd semantics of the
-    reference modules: ReLU grad where output > 0; sigmoid grad y(1-y))."""
+    reference modules: ReLU grad where output > 0; sigmoid grad y(1-y)). Every parameter gradient is a sum over the
+    points; abs_terms=True also returns, per gradient element, the sum of the ABSOLUTE values of its terms (float64),
+    the scale of the fp32 summation-order error any implementation's sum of those terms carries (parity_gates.SUM_REL)."""
     R, P = cache.n_rays, cache.P
     N = R * P
     gs = g_sigma.reshape(N, 1).astype(f32)
     gr = g_rgb.reshape(N, -1).astype(f32)
     grads: Dict[str, np.ndarray] = {}
+    absg: Dict[str, np.ndarray] = {}
+
+    def a(x):
+        return np.abs(np.asarray(x, np.float64))
+
+    def reduce(name, g, x=None):  # grads[name] = g^T x (or the column sums of g), and its |terms| sums
+        grads[name] = (g.T @ x).astype(f32) if x is not None else g.sum(0).astype(f32)
+        if abs_terms:
+            absg[name] = a(g).T @ a(x) if x is not None else a(g).sum(0)
+
     rgb = cache.rgb
     gu = (gr * (f32(1.0) - rgb) * rgb).astype(f32)
-    grads["color_layer.2.weight"] = (gu.T @ cache.c0).astype(f32)
-    grads["color_layer.2.bias"] = gu.sum(0).astype(f32)
+    reduce("color_layer.2.weight", gu, cache.c0)
+    reduce("color_layer.2.bias", gu)
     gc0 = (gu @ params["color_layer.2.weight"]).astype(f32)
     gz = np.where(cache.c0 > 0 if cache.color_mask is None else cache.color_mask, gc0, f32(0.0)).astype(f32)
     n1 = cache.inter.shape[-1]
@@ -274,24 +287,27 @@ def nerf_mlp_backward(params: Dict[str, np.ndarray], arch: MLPArch, cache: MLPCa
     gz_ray = gz.reshape(R, P, -1).sum(1).astype(f32)
     gW2 = (gz_ray.T @ cache.dir_embed).astype(f32)
     grads["color_layer.0.weight"] = np.concatenate([gW1, gW2], 1)
-    grads["color_layer.0.bias"] = gz.sum(0).astype(f32)
+    if abs_terms:
+        absg["color_layer.0.weight"] = np.concatenate(
+            [a(gz).T @ a(cache.inter), a(gz).reshape(R, P, -1).sum(1).T @ a(cache.dir_embed)], 1)
+    reduce("color_layer.0.bias", gz)
     g_inter = (gz @ params["color_layer.0.weight"][:, :n1]).astype(f32)
-    grads["intermediate_linear.weight"] = (g_inter.T @ cache.features).astype(f32)
-    grads["intermediate_linear.bias"] = g_inter.sum(0).astype(f32)
-    grads["density_layer.weight"] = (gs.T @ cache.features).astype(f32)
-    grads["density_layer.bias"] = gs.sum(0).astype(f32)
+    reduce("intermediate_linear.weight", g_inter, cache.features)
+    reduce("intermediate_linear.bias", g_inter)
+    reduce("density_layer.weight", gs, cache.features)
+    reduce("density_layer.bias", gs)
     gy = (g_inter @ params["intermediate_linear.weight"] + gs @ params["density_layer.weight"]).astype(f32)
     for li in reversed(range(arch.n_layers)):
         y = cache.layer_out[li]
         gzl = np.where(y > 0 if cache.trunk_masks is None else cache.trunk_masks[li], gy, f32(0.0)).astype(f32)
         W = params[f"xyz_encoder.mlp.{li}.0.weight"]
-        grads[f"xyz_encoder.mlp.{li}.0.weight"] = (gzl.T @ cache.layer_in[li]).astype(f32)
-        grads[f"xyz_encoder.mlp.{li}.0.bias"] = gzl.sum(0).astype(f32)
+        reduce(f"xyz_encoder.mlp.{li}.0.weight", gzl, cache.layer_in[li])
+        reduce(f"xyz_encoder.mlp.{li}.0.bias", gzl)
         if li == 0:
             break
         gin = (gzl @ W).astype(f32)
         gy = gin[:, : gin.shape[1] - cache.embed.shape[1]] if li in arch.input_skips else gin
-    return grads
+    return (grads, absg) if abs_terms else grads
 
 
 # ============================================================================ raymarcher
@@ -500,9 +516,10 @@ def render_two_pass(params_c, params_f, arch, cfg: RenderCfg, origins, direction
 
 
 def train_step_grads(params_c, params_f, arch, cfg: RenderCfg, origins, directions, lengths, gt_rgb,
-                     noise_c, noise_f, pdf_u, z_fine=None, relu_masks=None):
+                     noise_c, noise_f, pdf_u, z_fine=None, relu_masks=None, abs_terms: bool = False):
     """One training step's objective and parameter gradients (nerf_pipeline.py:181-213, 284-305; apis.py:87-88):
-    objective = mse(fine) + mse(coarse); noise_* already include density_noise_std."""
+    objective = mse(fine) + mse(coarse); noise_* already include density_noise_std. abs_terms=True adds each gradient
+    element's sum of absolute term values (abs_fine / abs_coarse, nerf_mlp_backward)."""
     R = lengths.shape[0]
     out = render_two_pass(params_c, params_f, arch, cfg, origins, directions, lengths, noise_c=noise_c,
                           noise_f=noise_f, pdf_u=pdf_u, random_sampling=True, z_fine=z_fine,
@@ -511,11 +528,16 @@ def train_step_grads(params_c, params_f, arch, cfg: RenderCfg, origins, directio
     mse_f = rgb_metrics(gt[None], out["fine"][0][None])["rgb_mse"]
     mse_c = rgb_metrics(gt[None], out["coarse"][0][None])["rgb_mse"]
     scale = f32(2.0 / (R * 3))
-    grads = []
+    grads, absg = [], []
     for stage, params, cache, ctx in (("fine", params_f, out["cache_f"], out["ctx_f"]),
                                       ("coarse", params_c, out["cache_c"], out["ctx_c"])):
         g_feat = ((out[stage][0] - gt) * scale).astype(f32)
         g_dens, g_cols = raymarch_backward(ctx, g_feat)
-        grads.append(nerf_mlp_backward(params, arch, cache, g_dens, g_cols))
-    return dict(objective=float(mse_f[0] + mse_c[0]), loss_rgb_mse=mse_f, loss_prev_stage_rgb_mse=mse_c,
-                grads_fine=grads[0], grads_coarse=grads[1], render=out)
+        r = nerf_mlp_backward(params, arch, cache, g_dens, g_cols, abs_terms=abs_terms)
+        grads.append(r[0] if abs_terms else r)
+        absg.append(r[1] if abs_terms else None)
+    res = dict(objective=float(mse_f[0] + mse_c[0]), loss_rgb_mse=mse_f, loss_prev_stage_rgb_mse=mse_c,
+               grads_fine=grads[0], grads_coarse=grads[1], render=out)
+    if abs_terms:
+        res.update(abs_fine=absg[0], abs_coarse=absg[1])
+    return res

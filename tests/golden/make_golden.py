@@ -40,7 +40,7 @@ _six = types.ModuleType("torch._six")
 _six.string_classes = (str, bytes)
 sys.modules.setdefault("torch._six", _six)
 
-from weights import LEGO_ARCH, SMALL_ARCH, checksum, make_nerf_mlp_params  # noqa: E402
+from weights import LEGO_ARCH, SMALL_ARCH, checksum, load_trained_params, make_nerf_mlp_params  # noqa: E402
 from scene import synthetic_pose  # noqa: E402
 
 from yanerf.pipelines.builder import PIPELINES  # noqa: E402
@@ -266,9 +266,14 @@ def lego_pipeline_cfg(n_fine=128, noise=0.2, n_rays=4096, H=800, W=800, focal_im
 
 
 def load_pipeline_weights(pipe, seeds):
-    for f, seed in zip(pipe.implicit_functions, seeds):
-        params = make_nerf_mlp_params(LEGO_ARCH, seed)
-        f._fn.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()})
+    """seeds: one PCG64 seed per MLP (make_nerf_mlp_params), or the string "trained" (trained_weights.npz)."""
+    params = load_trained_params() if isinstance(seeds, str) else [make_nerf_mlp_params(LEGO_ARCH, s) for s in seeds]
+    for f, p in zip(pipe.implicit_functions, params):
+        f._fn.load_state_dict({k: torch.from_numpy(v) for k, v in p.items()})
+
+
+def seeds_field(seeds):
+    return np.str_(seeds) if isinstance(seeds, str) else np.array(list(seeds))
 
 
 def gen_render_eval(out):
@@ -354,7 +359,8 @@ def record_train_step(pcfg, seeds, pose, focal, img, n_rays, torch_seed, min_dep
     preds["objective"].mean().backward()
     ids = rec.take("multinomial")[0].numpy().astype(np.int64)
     assert len(refined) == 1
-    d = dict(pose=np32(pose), focal=np32(focal), seeds=np.array(list(seeds)), n_rays=np.int64(n_rays),
+    d = dict(pose=np32(pose), focal=np32(focal), seeds=seeds_field(seeds), n_rays=np.int64(n_rays),
+             H=np.int64(pcfg.ray_sampler.image_height), W=np.int64(pcfg.ray_sampler.image_width),
              pixel_ids=ids, gt_rgb=np32(img.reshape(1, -1, 3)[0, ids[0]]),
              jitter_u=np32(rec.take("rand_like")[0]),
              pdf_u=np32(rec.take("rand")[0]),
@@ -479,6 +485,10 @@ def gen_sensitivity(out):
         cases.append((f"fern_{n_fine}", fern_pipeline_cfg(n_fine), (41, 42), torch.from_numpy(forward_pose())[None],
                       torch.tensor([FERN_FOCAL]), 9, 12,
                       dict(min_depth=torch.tensor([[FERN_NEAR]]), max_depth=torch.tensor([[FERN_FAR]]))))
+    cases.append(("trained", lego_pipeline_cfg(H=TRAINED_HW, W=TRAINED_HW), "trained", torch.from_numpy(TRAINED_POSE)[None],
+                  torch.tensor([TRAINED_FOCAL], dtype=torch.float32), TRAINED_GRID, TRAINED_GRID, {}))
+    if os.environ.get("YANERF_SENSITIVITY_ONLY"):
+        cases = [c for c in cases if c[0] == os.environ["YANERF_SENSITIVITY_ONLY"]]
 
     def ulp(a, rng):
         up = rng.integers(0, 2, size=a.shape).astype(bool)
@@ -537,6 +547,44 @@ def gen_sensitivity(out):
             trials=np.int64(20), max_z_move=dz.astype(np.float32), max_rgb_move=drgb.astype(np.float32),
             z_fine=base["z_fine"], fine_features=base["fine_features"], z_fine_f64=r64["z_fine"].astype(np.float64),
             fine_features_f64=r64["fine_features"].astype(np.float64))
+
+
+# Parity at TRAINED weights: the Lego architecture trained 1,500 fused fp32 steps (tools/density_collapse_probe.py: seed
+# 7, density-layer bias 1.0 at init, 4096 rays, 64 + 128, test PSNR 36.9 dB, profiles/r4_density_collapse_probe.jsonl)
+# on the procedural scene of tools/synthetic_scene.py (100 x 100 views, camera radius 4, lego.yml's near / far),
+# model tensors of its checkpoint saved as trained_weights.npz. Its density is peaked at the scene's surfaces, so
+# sample_pdf is far better conditioned than at random init (the other goldens' weights). (With the reference's zero
+# density bias, nerf_mlp.py:69-71, this scene's training collapses to the transparent solution for seeds 42 and 1.)
+TRAINED_HW, TRAINED_GRID = 100, 25
+TRAINED_POSE = synthetic_pose(45.0, -30.0, 4.0)
+TRAINED_FOCAL = 0.5 * TRAINED_HW / np.tan(0.5 * 0.6911112070083618)  # synthetic_scene.CAMERA_ANGLE_X
+
+
+def scene_view(theta, phi, hw):
+    """The procedural scene's ground-truth RGB at one camera (tools/synthetic_scene.render_view, black background)."""
+    sys.path.insert(0, str(HERE.parents[1] / "tools"))
+    from synthetic_scene import pose_spherical, render_view
+    return render_view(pose_spherical(theta, phi, 4.0), hw, hw)[..., :3]
+
+
+def gen_render_trained(out):
+    pipe = PIPELINES.build(lego_pipeline_cfg(H=TRAINED_HW, W=TRAINED_HW))
+    load_pipeline_weights(pipe, "trained")
+    pipe.eval()
+    pose, focal = torch.from_numpy(TRAINED_POSE)[None], torch.tensor([TRAINED_FOCAL], dtype=torch.float32)
+    d = record_eval_render(pipe, pose, focal, TRAINED_GRID, TRAINED_GRID)
+    d.update(pose=np32(pose), focal=np32(focal), H=np.int64(TRAINED_GRID), W=np.int64(TRAINED_GRID),
+             cfg_hw=np.int64(TRAINED_HW), seeds=seeds_field("trained"))
+    out["render_trained"] = d
+
+
+def gen_train_step_trained(out):
+    n_rays = 64
+    pcfg = lego_pipeline_cfg(n_rays=n_rays, H=TRAINED_HW, W=TRAINED_HW)
+    pose = torch.from_numpy(synthetic_pose(-70.0, -25.0, 4.0))[None]
+    focal = torch.tensor([TRAINED_FOCAL], dtype=torch.float32)
+    img = torch.from_numpy(np.ascontiguousarray(scene_view(-70.0, -25.0, TRAINED_HW)))[None].float()
+    out["train_step_trained"] = record_train_step(pcfg, "trained", pose, focal, img, n_rays, torch_seed=31)
 
 
 def gen_zero_outputer(out):
@@ -772,7 +820,8 @@ def gen_iter_runner(out):
 
 GENERATORS = (gen_harmonic, gen_raysampler, gen_mlp, gen_raymarcher, gen_sample_pdf, gen_render_eval,
               gen_train_step, gen_zero_outputer, gen_init_checksums, gen_pipeline_state, gen_lr_schedule,
-              gen_raysampler_masked, gen_iter_runner, gen_render_fern, gen_train_step_fern, gen_sensitivity)
+              gen_raysampler_masked, gen_iter_runner, gen_render_fern, gen_train_step_fern, gen_sensitivity,
+              gen_render_trained, gen_train_step_trained)
 
 
 def main():

@@ -80,3 +80,16 @@ def make_nerf_mlp_params(arch: dict, seed: int, density_bias: float = 0.1) -> Di
 
 def checksum(params: Dict[str, np.ndarray]) -> np.ndarray:
     return np.array([float(np.sum(params[k].astype(np.float64))) for k in sorted(params)], dtype=np.float64)
+
+
+def load_trained_params(path=None) -> List[Dict[str, np.ndarray]]:
+    """The two trained Lego-architecture MLPs (coarse, fine) of trained_weights.npz, reference state_dict names
+    (keys `implicit_functions.{i}._fn.<name>` in the file; see make_golden.py TRAINED_*)."""
+    from pathlib import Path
+    path = Path(path) if path else Path(__file__).resolve().parent / "trained_weights.npz"
+    out: List[Dict[str, np.ndarray]] = [{}, {}]
+    with np.load(path, allow_pickle=False) as z:
+        for k in z.files:
+            i, name = int(k.split(".")[1]), k.split("._fn.", 1)[1]
+            out[i][name] = z[k].astype(np.float32)
+    return out

@@ -25,6 +25,8 @@ import os
 import time
 from pathlib import Path
 
+from contextlib import contextmanager
+
 import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
@@ -65,9 +67,14 @@ def reference_sensitive_rays(sens, z_tol=2e-5):
 
 
 def split_gate(rgb, rgb_ref, z, z_ref, depth=None, depth_ref=None, *, fine_at=None, coarse=None, strict=1e-5,
-               strict_depth=1e-4, z_tol=2e-5, tag="", sensitivity=None):
+               strict_depth=1e-4, z_tol=2e-5, tag="", sensitivity=None, same_tol=None, same_tol_depth=None,
+               all_vs_oracle=False):
     """coarse = (O, lengths [R,Pc], our coarse weights [R,Pc], n_fine): the oracle refinement of our coarse weights
     (deterministic, as the evaluation pass runs it) must equal z on every ray.
+    same_tol / same_tol_depth: the bound on the rays whose refined depths agree with the reference's to z_tol (default
+    strict / strict_depth). all_vs_oracle: every ray (not only those with other depths) is also held to strict /
+    strict_depth against the oracle's fine stage at OUR refined depths -- for a sharp trained density, where depths
+    equal to z_tol still move the colour by more than `strict` (the looser same_tol then bounds that effect).
     sensitivity = the reference's own sensitivity golden of this render (reference_sensitive_rays): the number of rays
     whose refined depths differ between this build and the reference must not exceed the number the reference itself
     moves under ulp-level changes of its coarse stage; the rays outside that set are counted in the report."""
@@ -105,11 +112,22 @@ def split_gate(rgb, rgb_ref, z, z_ref, depth=None, depth_ref=None, *, fine_at=No
         if depth is not None:
             report["max_depth_err_other_depths_vs_oracle_at_our_depths"] = float(
                 np.abs(depth[flip] - np.asarray(d_o, np.float64)).max())
+    if all_vs_oracle:
+        rows = np.arange(R)
+        f_a, d_a = fine_at(rows, z)
+        report["max_rgb_err_all_vs_oracle_at_our_depths"] = float(
+            np.abs(rgb - np.asarray(f_a, np.float64).reshape(R, -1)).max())
+        if depth is not None:
+            report["max_depth_err_all_vs_oracle_at_our_depths"] = float(np.abs(depth - np.asarray(d_a, np.float64)).max())
     print(f"split_gate {tag}: {report}")
     write_report("split_gate", tag, report)
-    assert report["max_rgb_err_same_depths"] <= strict, report
+    assert report["max_rgb_err_same_depths"] <= (strict if same_tol is None else same_tol), report
     if depth is not None:
-        assert report["max_depth_err_same_depths"] <= strict_depth, report
+        assert report["max_depth_err_same_depths"] <= (strict_depth if same_tol_depth is None else same_tol_depth), report
+    if all_vs_oracle:
+        assert report["max_rgb_err_all_vs_oracle_at_our_depths"] <= strict, report
+        if depth is not None:
+            assert report["max_depth_err_all_vs_oracle_at_our_depths"] <= strict_depth, report
     if coarse is not None:
         assert report["max_depth_err_vs_oracle_refine_of_our_weights"] <= z_tol, report
     if sensitivity is not None:
@@ -121,6 +139,65 @@ def split_gate(rgb, rgb_ref, z, z_ref, depth=None, depth_ref=None, *, fine_at=No
         if depth is not None:
             assert report["max_depth_err_other_depths_vs_oracle_at_our_depths"] <= strict_depth, report
     return report
+
+
+# fp32 summation order. Every parameter-gradient element is a sum over the step's points (up to ~25k terms here), and
+# two correct fp32 evaluations summing the same terms in different orders differ by up to ~n * 2^-24 * sum|terms|.
+# Where a sum cancels (sum|terms| >> |sum|: the density-layer bias at the trained weights, kappa ~15) that difference
+# alone can exceed 1e-4 * max|ref| with both sides correct -- there the reference's own value sits 7.8e-6 * sum|terms|
+# from the exact (float64) sum of its terms, 1.1e-4 of its magnitude. Every strict gradient gate therefore allows, per
+# element, SUM_REL * sum|terms| on top of its relative bound (sum|terms| from the oracle, nerf_mlp_backward abs_terms),
+# and reports how many elements needed it ("sum_limited").
+SUM_REL = 2e-5
+
+
+def _flat(x, idx=None):
+    x = np.asarray(x, np.float64).reshape(-1)
+    return x if idx is None else x[idx]
+
+
+# an fp32 implementation's gradients may be at most this much further from the exact (float64) algorithm than the
+# reference's own fp32 gradients are (or within STRICT_GRAD of it)
+EXACT_RATIO = 1.5
+
+
+@contextmanager
+def float64_oracle(O):
+    """Run the oracle in float64 (its arithmetic type is the module global `f32`): the reference's algorithm without
+    fp32 rounding, the common yardstick for how far each fp32 implementation (the reference, the oracle, HIP) lands
+    from the exact result."""
+    old = O.f32
+    O.f32 = np.float64
+    try:
+        yield O
+    finally:
+        O.f32 = old
+
+
+def max_rel_vs(models_or_items, exact) -> float:
+    """max over tensors of max |x - exact| / max |exact| (exact: {name: array}); items are (name, array) pairs."""
+    worst = 0.0
+    for name, x in models_or_items:
+        e = np.asarray(exact[name], np.float64).reshape(-1)
+        x = np.asarray(x, np.float64).reshape(-1)
+        worst = max(worst, float(np.abs(x - e).max() / max(np.abs(e).max(), 1e-30)))
+    return worst
+
+
+def strict_grad_gate(v, ref, abs_terms=None, name="", tol: float = STRICT_GRAD) -> dict:
+    """|v - ref| <= tol * max|ref| + SUM_REL * sum|terms| for every element (abs_terms None: the relative bound alone).
+    Returns {err: max |v - ref| / max|ref|, sum_limited: elements beyond tol * max|ref|}."""
+    v, ref = _flat(v), _flat(ref)
+    M = max(np.abs(ref).max(), 1e-30)
+    err = np.abs(v - ref)
+    allow = tol * M + (SUM_REL * _flat(abs_terms) if abs_terms is not None else 0.0)
+    over = err > tol * M
+    # the share of the summation allowance used by the worst element beyond the relative bound (0..1)
+    rep = dict(err=float(err.max() / M), sum_limited=int(over.sum()),
+               sum_allowance_used=float(((err - tol * M)[over] / np.maximum(SUM_REL * _flat(abs_terms)[over], 1e-300))
+                                        .max()) if abs_terms is not None and over.any() else 0.0)
+    assert (err <= allow).all(), (name, rep)
+    return rep
 
 
 def grad_err(v, ref) -> float:
@@ -160,7 +237,8 @@ def golden_grad_items(g, models):
                 yield i, name, v[idx], g[f"gradval{i}:{name}"].astype(np.float64), idx
 
 
-def tie_budget_gate(v, ref, o_hip, o_ref, name, strict: float = STRICT_GRAD, pin: float = ORACLE_PIN) -> dict:
+def tie_budget_gate(v, ref, o_hip, o_ref, name, strict: float = STRICT_GRAD, pin: float = ORACLE_PIN,
+                    abs_terms=None) -> dict:
     """The direct comparison with the reference's gradient, strict per element with the ReLU ties (and, for a fine pass
     at this build's own refined depths, the sample_pdf flips) as an explicit budget:
 
@@ -170,18 +248,24 @@ def tie_budget_gate(v, ref, o_hip, o_ref, name, strict: float = STRICT_GRAD, pin
     O_ref = the same under the reference's own recorded decisions (at the reference's depths), itself pinned to the
     reference (|O_ref - reference| <= pin * max, asserted here). |O_hip - O_ref| is exactly what the differing decisions
     (fp32 ties at the kink, flipped samples) contribute; whatever ours differs by beyond it must be within `strict`.
-    Returns {direct, budget, residual, pin}: max |ours - ref|, max |O_hip - O_ref|, max (|ours - ref| - |O_hip - O_ref|)
-    and max |O_ref - ref|, each relative to max |ref|."""
+    Both bounds also allow SUM_REL * sum|terms| per element (abs_terms: the oracle's, under the reference's decisions),
+    the fp32 summation-order term (see SUM_REL). Returns {direct, budget, residual, pin, sum_limited}: max |ours - ref|,
+    max |O_hip - O_ref|, max (|ours - ref| - |O_hip - O_ref|) and max |O_ref - ref|, each relative to max |ref|, and
+    the number of elements beyond the relative bounds alone."""
     v, ref, o_hip, o_ref = (np.asarray(x, np.float64).reshape(-1) for x in (v, ref, o_hip, o_ref))
     M = max(np.abs(ref).max(), 1e-30)
-    pin_err = float(np.abs(o_ref - ref).max() / M)
-    assert pin_err <= pin, (name, "oracle under the reference's decisions vs the reference", pin_err)
+    slack = SUM_REL * _flat(abs_terms) if abs_terms is not None else 0.0
+    pin_abs = np.abs(o_ref - ref)
+    pin_err = float(pin_abs.max() / M)
+    assert (pin_abs <= pin * M + slack).all(), (name, "oracle under the reference's decisions vs the reference", pin_err)
     budget = np.abs(o_hip - o_ref)
     direct = np.abs(v - ref)
     excess = direct - budget
+    over = excess > strict * M
     rep = dict(direct=float(direct.max() / M), budget=float(budget.max() / M),
-               residual=float(max(excess.max(), 0.0) / M), pin=pin_err)
-    assert excess.max() <= strict * M, (name, rep)
+               residual=float(max(excess.max(), 0.0) / M), pin=pin_err,
+               sum_limited=int(over.sum()), pin_sum_limited=int((pin_abs > pin * M).sum()))
+    assert (excess <= strict * M + slack).all(), (name, rep)
     return rep
 
 
@@ -195,6 +279,8 @@ def summarize_tie_budget(per_tensor: dict) -> dict:
         out[f"{tag}_tie_budget_max"] = max(r["budget"] for r in rows)
         out[f"{tag}_residual_max"] = max(r["residual"] for r in rows)
         out[f"{tag}_oracle_pin_max"] = max(r["pin"] for r in rows)
+        out[f"{tag}_sum_limited_elements"] = sum(r.get("sum_limited", 0) for r in rows)
+        out[f"{tag}_pin_sum_limited_elements"] = sum(r.get("pin_sum_limited", 0) for r in rows)
     out["per_tensor"] = {f"{k[0]}:{k[1]}": {kk: float(f"{vv:.3e}") for kk, vv in r.items()}
                          for k, r in per_tensor.items()}
     return out

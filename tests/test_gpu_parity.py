@@ -12,8 +12,8 @@ import pytest
 import torch
 
 from oracle import nerf_oracle as O
-from parity_gates import (golden_grad_items, golden_relu_masks, grad_err, hip_relu_masks, loose_grad_gate,
-                          oracle_fine_at, split_gate, summarize_tie_budget, tie_budget_gate, write_report)
+from parity_gates import (golden_grad_items, golden_relu_masks, hip_relu_masks, loose_grad_gate, oracle_fine_at,
+                          split_gate, summarize_tie_budget, tie_budget_gate, write_report)
 from weights import LEGO_ARCH, SMALL_ARCH, make_nerf_mlp_params
 
 pytestmark = pytest.mark.gpu
@@ -450,15 +450,16 @@ def test_train_step_lego(pkg, golden, precision, depths):
               (g["noise_fine"] * np.float32(0.2)).astype(np.float32), g["pdf_u"])
     o_hip = O.train_step_grads(*args, *inputs, z_fine=z_ours, relu_masks=tuple(masks))
     o_ref = O.train_step_grads(*args, *inputs, z_fine=g["z_fine"],
-                               relu_masks=(golden_relu_masks(g, 0), golden_relu_masks(g, 1)))
+                               relu_masks=(golden_relu_masks(g, 0), golden_relu_masks(g, 1)), abs_terms=True)
     budget = {}
     loose = 0.0
     for i, name, v, ref, idx in golden_grad_items(g, [f._fn for f in pipe.implicit_functions]):
-        key = "grads_coarse" if i == 0 else "grads_fine"
-        oh, orf = (np.asarray(x[key][name], np.float64).reshape(-1) for x in (o_hip, o_ref))
+        key = "coarse" if i == 0 else "fine"
+        oh, orf, ab = (np.asarray(x, np.float64).reshape(-1) for x in
+                       (o_hip[f"grads_{key}"][name], o_ref[f"grads_{key}"][name], o_ref[f"abs_{key}"][name]))
         if idx is not None:
-            oh, orf = oh[idx], orf[idx]
-        budget[(i, name)] = tie_budget_gate(v, ref, oh, orf, f"{i}:{name}")
+            oh, orf, ab = oh[idx], orf[idx], ab[idx]
+        budget[(i, name)] = tie_budget_gate(v, ref, oh, orf, f"{i}:{name}", abs_terms=ab)
         loose = max(loose, loose_grad_gate(v, ref, name, enforce=False))
     write_report("train_step", f"registry lego {precision} depths={depths}",
                  dict(grad_worst_rel_l2_vs_reference=loose, tie_budget=summarize_tie_budget(budget)))

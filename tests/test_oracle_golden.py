@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from oracle import nerf_oracle as O
-from weights import LEGO_ARCH, SMALL_ARCH, checksum, make_nerf_mlp_params
+from weights import LEGO_ARCH, SMALL_ARCH, checksum, load_trained_params, make_nerf_mlp_params
 
 
 def close(a, b, atol, rtol=0.0):
@@ -188,33 +188,64 @@ def test_conditional_mlp(golden):
         np.testing.assert_allclose(rgb, g["rgb"][b], atol=2e-6)
 
 
-def test_train_step_lego_strict_under_reference_relu_decisions(golden):
+def golden_params(g):
+    """(coarse, fine) parameters of a golden: PCG64 seeds, or "trained" (trained_weights.npz)."""
+    if g["seeds"].dtype.kind == "U":
+        return load_trained_params()
+    return [make_nerf_mlp_params(LEGO_ARCH, int(s)) for s in g["seeds"]]
+
+
+@pytest.mark.parametrize("case", ["train_step_lego", "train_step_trained"])
+def test_train_step_lego_strict_under_reference_relu_decisions(golden, case):
     """The oracle's training step at the reference's refined depths and under the reference's own ReLU decisions
     (both recorded in the golden): every gradient element of both MLPs within 1e-4 * max of the reference's (measured
     7.5e-6 coarse, 1.6e-5 fine). Where the oracle's own signs differ from the reference's, the pre-activation is an fp32
-    tie (parity_gates.relu_ties; measured: 10 units, all within 6e-6 of zero relative to their layer)."""
-    from parity_gates import STRICT_GRAD, TIE_REL, golden_relu_masks, grad_err, relu_ties
-    g = golden("train_step_lego")
+    tie (parity_gates.relu_ties; measured: 10 units, all within 6e-6 of zero relative to their layer). case
+    "train_step_trained": the same at the trained weights (64 rays of the procedural scene's 100 x 100 camera)."""
+    from parity_gates import TIE_REL, golden_relu_masks, relu_ties, strict_grad_gate
+    g = golden(case)
     arch = O.MLPArch.from_dict(LEGO_ARCH)
-    pc, pf = (make_nerf_mlp_params(LEGO_ARCH, int(s)) for s in g["seeds"])
-    o, d, t, xy = O.sample_rays_train(g["pose"], g["focal"], 800, 800, 2.0, 6.0, 64, g["pixel_ids"], g["jitter_u"])
+    pc, pf = golden_params(g)
+    hw = int(g["H"]) if "H" in g else 800
+    o, d, t, xy = O.sample_rays_train(g["pose"], g["focal"], hw, hw, 2.0, 6.0, 64, g["pixel_ids"], g["jitter_u"])
     R = int(g["n_rays"])
     masks = (golden_relu_masks(g, 0), golden_relu_masks(g, 1))
     res = O.train_step_grads(pc, pf, arch, _lego_cfg(0.2), o.reshape(R, 3), d.reshape(R, 3), t.reshape(R, 64),
                              g["gt_rgb"], (g["noise_coarse"] * np.float32(0.2)).astype(np.float32),
                              (g["noise_fine"] * np.float32(0.2)).astype(np.float32), g["pdf_u"], z_fine=g["z_fine"],
-                             relu_masks=masks)
-    for i, key in ((0, "grads_coarse"), (1, "grads_fine")):
-        for k, v in res[key].items():
+                             relu_masks=masks, abs_terms=True)
+    for i, key in ((0, "coarse"), (1, "fine")):
+        for k, v in res[f"grads_{key}"].items():
+            a = res[f"abs_{key}"][k]
             if f"grad{i}:{k}" in g:
-                e = grad_err(v, g[f"grad{i}:{k}"])
+                strict_grad_gate(v, g[f"grad{i}:{k}"], a, (i, k))
             else:
-                e = grad_err(v.reshape(-1)[g[f"gradidx{i}:{k}"]], g[f"gradval{i}:{k}"])
-            assert e <= STRICT_GRAD, (i, k, e)
+                idx = g[f"gradidx{i}:{k}"]
+                strict_grad_gate(v.reshape(-1)[idx], g[f"gradval{i}:{k}"], a.reshape(-1)[idx], (i, k))
+    close(res["objective"], g["objective"][0], 1e-6)
     for k, cache in ((0, res["render"]["cache_c"]), (1, res["render"]["cache_f"])):
         own = dict(trunk=[z > 0 for z in cache.layer_pre], color=cache.c0_pre > 0)
         n_ties, worst = relu_ties(own, masks[k], cache)
         assert worst <= TIE_REL, (k, n_ties, worst)
+
+
+def test_render_trained_stagewise(golden):
+    """The oracle against the reference's evaluation render at the TRAINED weights (render_trained.npz: the central
+    25 x 25 grid of the procedural scene's 100 x 100 camera): rays, the coarse stage, and the fine stage at the
+    reference's own refined depths (strict), so the trained-weights GPU parity tests rest on a pinned oracle."""
+    g = golden("render_trained")
+    arch = O.MLPArch.from_dict(LEGO_ARCH)
+    pc, pf = golden_params(g)
+    H, W, hw = int(g["H"]), int(g["W"]), int(g["cfg_hw"])
+    R = H * W
+    o, d, z, _ = O.sample_rays_eval(g["pose"], g["focal"], hw, hw, 2.0, 6.0, 64, H=H, W=W)
+    np.testing.assert_allclose(z.reshape(R, 64), g["lengths"], atol=1e-6, rtol=1e-7)
+    r = O.render_two_pass(pc, pf, arch, _lego_cfg(), o.reshape(R, 3), d.reshape(R, 3), z.reshape(R, 64),
+                          z_fine=g["z_fine"])
+    np.testing.assert_allclose(r["coarse"][0], g["coarse_features"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(r["coarse"][3], g["coarse_weights"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(r["fine"][0], g["fine_features"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(np.asarray(r["fine"][1]).reshape(R), g["fine_depths"], atol=1.5e-4, rtol=0)
 
 
 def test_tie_budget_gate_accounts_for_the_oracles_own_ties(golden):
@@ -242,14 +273,16 @@ def test_tie_budget_gate_accounts_for_the_oracles_own_ties(golden):
             (g["noise_coarse"] * np.float32(0.2)).astype(np.float32),
             (g["noise_fine"] * np.float32(0.2)).astype(np.float32), g["pdf_u"])
     own = O.train_step_grads(*args)
-    ref = O.train_step_grads(*args, z_fine=g["z_fine"], relu_masks=(golden_relu_masks(g, 0), golden_relu_masks(g, 1)))
+    ref = O.train_step_grads(*args, z_fine=g["z_fine"], relu_masks=(golden_relu_masks(g, 0), golden_relu_masks(g, 1)),
+                             abs_terms=True)
     worst = {}
     for i, name, v, r, idx in golden_grad_items(g, [_P(own["grads_coarse"]), _P(own["grads_fine"])]):
-        key = "grads_coarse" if i == 0 else "grads_fine"
-        oh, orf = (np.asarray(x[key][name], np.float64).reshape(-1) for x in (own, ref))
+        key = "coarse" if i == 0 else "fine"
+        oh, orf, ab = (np.asarray(x, np.float64).reshape(-1)
+                       for x in (own[f"grads_{key}"][name], ref[f"grads_{key}"][name], ref[f"abs_{key}"][name]))
         if idx is not None:
-            oh, orf = oh[idx], orf[idx]
-        rep = tie_budget_gate(v, r, oh, orf, f"{i}:{name}")
+            oh, orf, ab = oh[idx], orf[idx], ab[idx]
+        rep = tie_budget_gate(v, r, oh, orf, f"{i}:{name}", abs_terms=ab)
         worst[i] = max(worst.get(i, 0.0), rep["direct"])
     assert max(worst.values()) > 1e-4  # the direct errors the budget has to cover are real (not a vacuous gate)
 
@@ -275,7 +308,7 @@ def test_train_step_fern_strict_under_reference_relu_decisions(golden, n_fine):
     tensor depth bounds averaged as ray_sampler.py:280-283 does, no density noise): the rays, the objective, and under
     the reference's recorded ReLU decisions and refined depths every gradient element of both MLPs within the
     parity_gates.ORACLE_PIN the GPU tests' tie budget relies on; its own decisions differ only at fp32 ties."""
-    from parity_gates import ORACLE_PIN, TIE_REL, golden_grad_items, golden_relu_masks, grad_err, relu_ties
+    from parity_gates import ORACLE_PIN, TIE_REL, golden_grad_items, golden_relu_masks, relu_ties, strict_grad_gate
     g = golden(f"train_step_fern_{n_fine}")
     arch = O.MLPArch.from_dict(LEGO_ARCH)
     pc, pf = (make_nerf_mlp_params(LEGO_ARCH, int(s)) for s in g["seeds"])
@@ -285,7 +318,7 @@ def test_train_step_fern_strict_under_reference_relu_decisions(golden, n_fine):
     cfg = O.RenderCfg(n_pts_fine=n_fine, near=near, far=far, raymarch=O.RaymarchOpts(background_density_bias=1e-6))
     args = (pc, pf, arch, cfg, o.reshape(R, 3), d.reshape(R, 3), t.reshape(R, 64), g["gt_rgb"], None, None, g["pdf_u"])
     masks = (golden_relu_masks(g, 0), golden_relu_masks(g, 1))
-    res = O.train_step_grads(*args, z_fine=g["z_fine"], relu_masks=masks)
+    res = O.train_step_grads(*args, z_fine=g["z_fine"], relu_masks=masks, abs_terms=True)
     close(res["objective"], g["objective"][0], 1e-6)
     np.testing.assert_allclose(res["render"]["coarse"][3], g["coarse_weights"], atol=1e-6, rtol=0)
 
@@ -298,7 +331,8 @@ def test_train_step_fern_strict_under_reference_relu_decisions(golden, n_fine):
                 yield k, type("G", (), {"grad": _T(v)})()
 
     for i, name, v, ref, idx in golden_grad_items(g, [_M(res["grads_coarse"]), _M(res["grads_fine"])]):
-        assert grad_err(v, ref) <= ORACLE_PIN, (i, name, grad_err(v, ref))
+        ab = res["abs_coarse" if i == 0 else "abs_fine"][name].reshape(-1)
+        strict_grad_gate(v, ref, ab if idx is None else ab[idx], (i, name), tol=ORACLE_PIN)
     for k, cache in ((0, res["render"]["cache_c"]), (1, res["render"]["cache_f"])):
         own = dict(trunk=[z > 0 for z in cache.layer_pre], color=cache.c0_pre > 0)
         assert relu_ties(own, masks[k], cache)[1] <= TIE_REL, k

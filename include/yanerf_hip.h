@@ -16,6 +16,10 @@
  *     yanerf_last_error() (thread-local).
  *   - Floating point tensors are fp32, row-major and contiguous with the reference's shapes, so torch
  *     tensors pass through without copies. Index tensors are int64.
+ *   - Empty bundles (zero rays / points / elements) are valid, as empty tensors are in the reference: the call
+ *     returns 0 before touching its per-ray buffers, which may then be NULL (torch gives an empty CUDA tensor a
+ *     NULL data pointer). yanerf_mlp_backward with zero points writes all-zero parameter gradients (nn.Linear's
+ *     gradient over an empty batch); yanerf_scatter_rays with zero rays writes the background image.
  *   - Randomness: a counter-based Philox4x32-10 stream keyed by (seed, offset); every random draw can
  *     instead be INJECTED by passing the uniforms/normals the reference consumed (test mode).
  */

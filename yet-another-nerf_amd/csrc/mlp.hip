@@ -2729,6 +2729,25 @@ __global__ void dw_reduce_kernel(DwJobs jobs, const float* __restrict__ slab) {
 
 // ============================================================================================ host helpers
 static int num_params(const yanerf_mlp_desc* d) { return 2 * d->n_layers + 8; }
+// element count of parameter i in the reference's state_dict order (the shapes build_pack_jobs reads)
+static int64_t param_numel(const MlpLayout& L, int i) {
+  if (i < 2 * L.L) {
+    const int l = i / 2, nout = (l + 1 < L.L) ? 256 : L.hid;
+    const bool sk = (L.skip >> l) & 1u;
+    const int din = (l == 0) ? L.xyz_dim : (sk ? 256 + L.xyz_dim : 256);
+    return (i % 2 == 0) ? (int64_t)nout * din : nout;
+  }
+  switch (i - 2 * L.L) {
+    case 0: return (int64_t)L.hid * L.hid;                 // intermediate_linear.weight
+    case 1: return L.hid;                                   // intermediate_linear.bias
+    case 2: return L.hid;                                   // density_layer.weight [1][hid]
+    case 3: return 1;                                       // density_layer.bias
+    case 4: return (int64_t)L.hdir * (L.hid + L.dir_dim);   // color_layer.0.weight
+    case 5: return L.hdir;                                  // color_layer.0.bias
+    case 6: return (int64_t)L.cdim * L.hdir;                // color_layer.2.weight
+    default: return L.cdim;                                 // color_layer.2.bias
+  }
+}
 
 static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, const float* const* prm, PackJobs& J) {
   J.n = 0;
@@ -3160,9 +3179,9 @@ int yanerf_mlp_forward(const yanerf_mlp_desc* d, int precision, const void* pack
                        const float* directions, const float* lengths, int64_t R, int64_t P, float* sigma_raw,
                        float* rgb, void* saved, void* stream) {
   if (check_desc(d)) return 1;
-  YN_CHECK(packed && origins && directions && lengths && sigma_raw && rgb, "mlp_forward: null pointer");
   YN_CHECK(R >= 0 && P >= 1, "mlp_forward: bad sizes R=%lld P=%lld", (long long)R, (long long)P);
-  if (R == 0) return 0;
+  if (R == 0) return 0;  // an empty bundle: no outputs (its buffers may be NULL)
+  YN_CHECK(packed && origins && directions && lengths && sigma_raw && rgb, "mlp_forward: null pointer");
   MlpLayout L = make_layout(d, precision);
   if (precision == YANERF_PREC_F32)
     return launch_fwd<float>(L, precision, packed, origins, directions, lengths, R, P, sigma_raw, rgb, saved,
@@ -3188,9 +3207,22 @@ int yanerf_mlp_backward_phase(const yanerf_mlp_desc* d, int precision, const voi
                               float* const* grads, void* workspace, int phase, void* stream) {
   if (check_desc(d)) return 1;
   YN_CHECK(phase == 1 || phase == 2 || phase == 3 || phase == 4 || phase == 8, "mlp_backward: bad phase %d", phase);
-  YN_CHECK(packed && saved && rgb && g_sigma && g_rgb && grads && workspace, "mlp_backward: null pointer");
+  YN_CHECK(R >= 0 && P >= 1, "mlp_backward: bad sizes R=%lld P=%lld", (long long)R, (long long)P);
+  YN_CHECK(grads, "mlp_backward: null pointer");
   for (int i = 0; i < num_params(d); ++i) YN_CHECK(grads[i], "mlp_backward: grad %d is null", i);
-  if (R * P == 0) return 0;
+  if (R == 0) {
+    // no points: every parameter gradient is an empty sum (torch's Linear backward over an empty batch gives zeros),
+    // written by the phases that write gradients (2, 3, 8); the point buffers may be NULL
+    if (phase == 2 || phase == 3 || phase == 8) {
+      const MlpLayout L = make_layout(d, precision);
+      for (int i = 0; i < num_params(d); ++i) {
+        const hipError_t e = hipMemsetAsync(grads[i], 0, (size_t)param_numel(L, i) * sizeof(float), as_stream(stream));
+        YN_CHECK(e == hipSuccess, "mlp_backward: zeroing grad %d failed: %s", i, hipGetErrorString(e));
+      }
+    }
+    return 0;
+  }
+  YN_CHECK(packed && saved && rgb && g_sigma && g_rgb && workspace, "mlp_backward: null pointer");
   MlpLayout L = make_layout(d, precision);
   if (precision == YANERF_PREC_F32)
     return launch_bwd<float>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R, P, grads, workspace,

@@ -788,8 +788,9 @@ int yanerf_raygen(const float* poses, const float* focal, const float* xy, const
                   int64_t P, int jitter_mode, const float* jitter_u, uint64_t seed, uint64_t offset, float* origins,
                   float* directions, float* lengths, float* xys, int64_t* ids_out, const float* bounds,
                   const uint64_t* rng_base, void* stream) {
-  YN_CHECK(poses && focal && origins && directions && xys && (lengths || P == 0), "yanerf_raygen: null pointer");
   YN_CHECK(B >= 0 && R >= 0 && P >= 0, "yanerf_raygen: negative size");
+  if (B * R == 0) return 0;  // empty bundles: nothing to read or write (their buffers may be NULL)
+  YN_CHECK(poses && focal && origins && directions && xys && (lengths || P == 0), "yanerf_raygen: null pointer");
   YN_CHECK(jitter_mode >= 0 && jitter_mode <= 2, "yanerf_raygen: bad jitter_mode %d", jitter_mode);
   YN_CHECK(jitter_mode != 1 || jitter_u, "yanerf_raygen: jitter_mode 1 needs jitter_u");
   if (!xy && !pixel_ids) YN_CHECK(R <= grid_w * grid_h, "yanerf_raygen: %lld rays > %lld pixels", (long long)R, (long long)(grid_w * grid_h));
@@ -820,8 +821,11 @@ int yanerf_composite_forward(const yanerf_raymarch_opts* o, const float* sigma_r
                              int64_t R, int64_t P, int64_t C, float* features, float* depths, float* alpha,
                              float* weights, void* stream) {
   if (composite_common(o, R, P, C)) return 1;
-  YN_CHECK(o->noise_mode != 1 || noise, "composite_forward: noise_mode 1 needs noise");
+  YN_CHECK(R >= 0, "composite_forward: negative size");
   if (R == 0) return 0;
+  YN_CHECK(sigma_raw && rgb && lengths && directions && features && depths && alpha && weights,
+           "composite_forward: null pointer");
+  YN_CHECK(o->noise_mode != 1 || noise, "composite_forward: noise_mode 1 needs noise");
   hipLaunchKernelGGL(composite_kernel<0>, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, as_stream(stream), *o,
                      sigma_raw, rgb, lengths, directions, bg, noise, R, P, C, features, depths, alpha, weights, nullptr,
                      nullptr, nullptr, nullptr, nullptr, CompositeLoss{});
@@ -834,9 +838,10 @@ int yanerf_composite_backward(const yanerf_raymarch_opts* o, const float* sigma_
                               const float* g_features, const float* g_depths, const float* g_alpha, int64_t R,
                               int64_t P, int64_t C, float* g_sigma, float* g_rgb, void* stream) {
   if (composite_common(o, R, P, C)) return 1;
+  YN_CHECK(R >= 0, "composite_backward: negative size");
+  if (R == 0) return 0;
   YN_CHECK(g_features && g_sigma && g_rgb, "composite_backward: null gradient pointer");
   YN_CHECK(o->noise_mode != 1 || noise, "composite_backward: noise_mode 1 needs noise");
-  if (R == 0) return 0;
   hipLaunchKernelGGL(composite_kernel<1>, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, as_stream(stream), *o,
                      sigma_raw, rgb, lengths, directions, bg, noise, R, P, C, nullptr, nullptr, nullptr, nullptr,
                      g_features, g_depths, g_alpha, g_sigma, g_rgb, CompositeLoss{});
@@ -852,11 +857,11 @@ int yanerf_composite_train(const yanerf_raymarch_opts* o, const float* sigma_raw
   YN_CHECK(B >= 1 && R % B == 0, "composite_train: %lld rays do not split over %lld images", (long long)R,
            (long long)B);
   if (composite_common(o, R, P, C)) return 1;
+  YN_CHECK(H > 0 && W > 0, "composite_train: image size %lld x %lld", (long long)H, (long long)W);
+  if (R == 0) return 0;
   YN_CHECK(features && depths && alpha && weights && g_sigma && g_rgb && image && xys,
            "composite_train: null pointer");
   YN_CHECK(o->noise_mode != 1 || noise, "composite_train: noise_mode 1 needs noise");
-  YN_CHECK(H > 0 && W > 0, "composite_train: image size %lld x %lld", (long long)H, (long long)W);
-  if (R == 0) return 0;
   const CompositeLoss loss{image, xys, R / B, H, W, scale, sq_err_per_ray, g_features};
   hipLaunchKernelGGL(composite_kernel<2>, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, as_stream(stream), *o,
                      sigma_raw, rgb, lengths, directions, bg, noise, R, P, C, features, depths, alpha, weights,
@@ -891,8 +896,9 @@ int yanerf_refine(const float* lengths, const float* ray_weights, int64_t R, int
 
 int yanerf_rgb_loss(const float* pred, const float* image, const float* xys, int64_t B, int64_t R, int64_t H,
                     int64_t W, int64_t C, float scale, float* sq_err_per_ray, float* g_pred, void* stream) {
-  YN_CHECK(pred && image && xys, "rgb_loss: null pointer");
+  YN_CHECK(B >= 0 && R >= 0, "rgb_loss: negative size");
   if (B * R == 0) return 0;
+  YN_CHECK(pred && image && xys && sq_err_per_ray, "rgb_loss: null pointer");
   int64_t n = B * R;
   hipLaunchKernelGGL(rgb_loss_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), pred, image,
                      xys, B, R, H, W, C, scale, sq_err_per_ray, g_pred);
@@ -902,8 +908,9 @@ int yanerf_rgb_loss(const float* pred, const float* image, const float* xys, int
 
 int yanerf_scatter_rays(const float* values, const float* xys, int64_t B, int64_t R, int64_t C, int64_t H, int64_t W,
                         const float* bg, float* out, void* stream) {
-  YN_CHECK(values && xys && out, "scatter_rays: null pointer");
   YN_CHECK(B >= 0 && R >= 0 && C >= 1 && H >= 1 && W >= 1, "scatter_rays: bad sizes");
+  YN_CHECK(out || B == 0, "scatter_rays: null output");
+  YN_CHECK((values && xys) || B * R == 0, "scatter_rays: null pointer");
   YN_CHECK(H * W < (1ll << 24), "scatter_rays: %lld pixels: the float pixel index is exact only below 2^24",
            (long long)(H * W));
   const int64_t n = B * H * W * C;
@@ -932,10 +939,11 @@ int yanerf_adam_scalars(double lr, double beta1, double beta2, int64_t step, flo
 
 int yanerf_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
                 double beta1, double beta2, double eps, double weight_decay, int64_t step, void* stream) {
-  YN_CHECK(params && grads && exp_avg && exp_avg_sq, "adam: null pointer");
+  YN_CHECK(n >= 0, "adam: negative size");
   float sc[2];
   if (yanerf_adam_scalars(lr, beta1, beta2, step, sc)) return 1;
   if (n == 0) return 0;
+  YN_CHECK(params && grads && exp_avg && exp_avg_sq, "adam: null pointer");
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), params, grads,
                      exp_avg, exp_avg_sq, n, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
                      (float)weight_decay, sc[0], sc[1]);
@@ -946,8 +954,9 @@ int yanerf_adam(float* params, const float* grads, float* exp_avg, float* exp_av
 int yanerf_adam_table(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                       const float* table, const int64_t* index, double beta1, double beta2, double eps,
                       double weight_decay, void* stream) {
-  YN_CHECK(params && grads && exp_avg && exp_avg_sq && table && index, "adam_table: null pointer");
+  YN_CHECK(n >= 0, "adam_table: negative size");
   if (n == 0) return 0;
+  YN_CHECK(params && grads && exp_avg && exp_avg_sq && table && index, "adam_table: null pointer");
   hipLaunchKernelGGL(adam_table_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), params,
                      grads, exp_avg, exp_avg_sq, n, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
                      (float)eps, (float)weight_decay, table, index);

@@ -508,6 +508,12 @@ DTYPES = {"fp32": "f32", "fp32x3": "f32 (3xbf16 split MFMA)",
 LEGO_TRAIN_IMAGES = 100  # nerf_synthetic Lego's train split (the loader length scripts/run.py:243-271 converts with)
 
 
+def progress(msg: str) -> None:
+    """A line on stderr per bench leg (rank 0): long runs keep writing, so a supervisor can tell them from a hang."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -632,6 +638,7 @@ def main():
     sec = [p for p in args.secondary.split(",") if p and p not in ("none", args.precision)]
     if sec:
         result["secondary"] = {}
+    progress("headline timed")
     for p2name in sec:
         tr2, dt2, _ = run(p2name, args.steps, args.warmup, probes=True)
         v2 = R * world * args.steps / dt2
@@ -660,13 +667,16 @@ def main():
     if not args.no_extras and world == 1:
         # single-GPU characteristics (evaluation render, drop-in path, other configs, graph replay): at N > 1 every rank
         # would repeat them, and the graph capture is single-rank by design
+        progress("extras")
         result["extras"] = extras(pcfg, cfg, dev, poses, focal, image, args.precision, tuple(sec))
     elif not args.no_extras:
         # BASELINE configs[3] / configs[4] on the same N ranks (the N-GPU half of those configs)
         result["configs_at_n"] = configs_at_n(pcfg, cfg, dev, poses, focal, image, world)
     if rank == 0 and world == 1 and args.psnr_steps > 0:
+        progress("psnr")
         result["psnr"] = psnr_leg(args.precision, args.psnr_steps, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(pcfg, Pc, Pf - Pc)
         result["vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
         result["reference_cpu"] = REFERENCE_CPU

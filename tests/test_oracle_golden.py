@@ -356,3 +356,44 @@ def test_render_fern_stagewise(golden, n_fine):
     np.testing.assert_allclose(r["coarse"][3], g["coarse_weights"], atol=1e-5, rtol=0)
     np.testing.assert_allclose(r["fine"][0], g["fine_features"], atol=1e-5, rtol=0)
     np.testing.assert_allclose(np.asarray(r["fine"][1]).reshape(R), g["fine_depths"], atol=1.5e-4, rtol=0)
+
+
+@pytest.mark.parametrize("case", ["train_step_lego", "train_step_trained"])
+def test_reference_and_oracle_fp32_gradients_vs_exact_algorithm(golden, case):
+    """The fp32 floor the gradient tolerances sit on: the oracle in float64 (parity_gates.float64_oracle, the
+    reference's algorithm without fp32 rounding) under the reference's decisions and depths, against the reference's
+    own recorded fp32 gradients and the fp32 oracle. Both fp32 implementations land ~1e-4 * max from the exact result
+    (measured: reference 4.6e-5 / 2.3e-4 coarse / fine at random init, 1.1e-4 / 7.7e-5 trained), which is what the GPU
+    tests' `ours_vs_exact <= max(1e-4, 1.5 * reference_vs_exact)` gate is calibrated against; and the float64 run
+    really is a different (more exact) evaluation, not the fp32 one."""
+    from parity_gates import float64_oracle, golden_relu_masks
+    g = golden(case)
+    arch = O.MLPArch.from_dict(LEGO_ARCH)
+    pc, pf = golden_params(g)
+    hw = int(g["H"]) if "H" in g else 800
+    o, d, t, _ = O.sample_rays_train(g["pose"], g["focal"], hw, hw, 2.0, 6.0, 64, g["pixel_ids"], g["jitter_u"])
+    R = int(g["n_rays"])
+    args = (pc, pf, arch, _lego_cfg(0.2), o.reshape(R, 3), d.reshape(R, 3), t.reshape(R, 64), g["gt_rgb"],
+            (g["noise_coarse"] * np.float32(0.2)).astype(np.float32),
+            (g["noise_fine"] * np.float32(0.2)).astype(np.float32), g["pdf_u"])
+    kw = dict(z_fine=g["z_fine"], relu_masks=(golden_relu_masks(g, 0), golden_relu_masks(g, 1)))
+    r32 = O.train_step_grads(*args, **kw)
+    with float64_oracle(O):
+        r64 = O.train_step_grads(*args, **kw)
+    assert O.f32 is np.float32  # restored
+    for i, key in ((0, "grads_coarse"), (1, "grads_fine")):
+        worst_ref = worst_o32 = 0.0
+        for k, ex in r64[key].items():
+            ex = np.asarray(ex, np.float64).reshape(-1)
+            v32 = np.asarray(r32[key][k], np.float64).reshape(-1)
+            if f"grad{i}:{k}" in g:
+                ref, e = g[f"grad{i}:{k}"].astype(np.float64).reshape(-1), ex
+                o32 = v32
+            else:
+                idx = g[f"gradidx{i}:{k}"]
+                ref, e, o32 = g[f"gradval{i}:{k}"].astype(np.float64), ex[idx], v32[idx]
+            M = np.abs(e).max()
+            worst_ref = max(worst_ref, float(np.abs(ref - e).max() / M))
+            worst_o32 = max(worst_o32, float(np.abs(o32 - e).max() / M))
+        assert 1e-6 < worst_ref <= 5e-4, (i, worst_ref)
+        assert 1e-6 < worst_o32 <= 5e-4, (i, worst_o32)

@@ -2790,19 +2790,27 @@ static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, const f
   return 0;
 }
 
-// point splits per dW tile: enough workgroups that the light jobs dispatched last fill the tail of the heavy ones
-// (fp32 / x3 at most 64; bf16 32: its fp8-MFMA dW is bound by the operand stream, and half the splits halve the slab
-// reduce, measured dW 0.87 -> 0.84 ms and reduce 0.036 -> 0.020 ms at the Lego fine pass); point-major: also enough
-// splits that one split's fp8 gradient scales fit the tile's PM_SCALES LDS slots
-constexpr int DW_SMAX = 64, DW_SMAX_PM = 32;
+// point splits per dW tile. fp32 / x3 (at most 64): enough workgroups that the light jobs dispatched last fill the
+// tail of the heavy ones (their grids are whole rounds of the 256 CUs: fp32 20 tiles x 64, x3 24 x 64).
+// bf16 (point-major, one 132 KB-LDS workgroup per CU, bound by its operand stream): whole rounds of one workgroup per
+// CU -- floor(256 / tiles) splits per round, as few rounds as the fp8 gradient scales allow (one split's scales must
+// fit the tile's PM_SCALES LDS slots). Lego fine pass (14 tiles): 18 splits = one round of 252 workgroups, dW 0.88-0.89
+// -> 0.79-0.81 ms and reduce 0.021 -> 0.016 ms against the former 32 splits (448 workgroups, 1.75 rounds); 36 (two
+// rounds) 0.84-0.86, 16 0.82-0.83, 24 / 28 0.90-0.98 (profiles/r4_ab_bf16_dw_splits.jsonl)
+constexpr int DW_SMAX = 64;
+constexpr int DW_CUS = 256;  // MI355X compute units
 static int dw_splits(int total_tiles, int64_t n_stages, bool pm) {
-  const int64_t smax = pm ? DW_SMAX_PM : DW_SMAX;
-  int64_t S = (smax * 64 + total_tiles - 1) / total_tiles;
-  if (S > n_stages) S = n_stages;
-  if (S > smax) S = smax;
+  int64_t S;
   if (pm) {
     const int64_t cap = (int64_t)(Cfg<bf16_t>::M / PM_SPTS) * (PM_SCALES - 2);  // stages per split whose scales fit
-    if (S < (n_stages + cap - 1) / cap) S = (n_stages + cap - 1) / cap;
+    const int64_t need = (n_stages + cap - 1) / cap;
+    const int64_t per_round = DW_CUS / total_tiles > 0 ? DW_CUS / total_tiles : 1;
+    S = per_round * (((need > 1 ? need : 1) + per_round - 1) / per_round);
+    if (S > n_stages) S = n_stages;  // (>= need)
+  } else {
+    S = (DW_SMAX * 64 + total_tiles - 1) / total_tiles;
+    if (S > n_stages) S = n_stages;
+    if (S > DW_SMAX) S = DW_SMAX;
   }
   if (S < 1) S = 1;
   return (int)S;

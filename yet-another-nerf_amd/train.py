@@ -148,8 +148,11 @@ class NeRFTrainer:
         # overlap: False = serial, True / "both" = the whole coarse backward on the side stream beside the fine one,
         # "split" = the coarse input-side walk (dX) first on the main stream, then its weight gradients (dW, a
         # byte-bound kernel) on the side stream beside the fine dX (an MFMA-bound kernel)
+        # Round 4, after the bf16 dW grid became one round of workgroups (tools/ab_overlap.py, bf16 step ms):
+        # serial 3.590, both 3.648, split 3.613, early 3.548 -> bf16 defaults to "early" (the coarse backward beside
+        # the refinement and the fine forward); fp32 serial 29.15 / early 29.15 / both 29.44 keeps serial.
         if overlap is None:
-            overlap = precision == "bf16"
+            overlap = "early" if precision == "bf16" else False
         self.overlap = "both" if overlap is True else overlap
         self.side = torch.cuda.Stream(device=self.dev) if overlap else None
         self.grad_exchange = grad_exchange or os.environ.get("YANERF_GRAD_EXCHANGE", "bucketed")

@@ -588,11 +588,11 @@ def main():
             # themselves) and, at N > 1, around the wait for the gradient exchange on the compute stream (its exposed
             # part); in the serial-backward modes at N = 1 the dX / dW / reduce launches too (the trainer then issues
             # the backward phase by phase). Its rate is reported beside the headline (`value_probed_window`)
-            # (under the "early" schedule, bf16's default at N = 1, the coarse backward runs beside the fine forward:
+            # (under the "early" schedule, bf16's default at every N, the coarse backward runs beside the fine forward:
             # that launch is then timed in the probe steps, alone on the GPU)
-            shares = tr.overlap == "early" and world == 1
-            names = ["mlp_fwd_0"] + ([] if shares else ["mlp_fwd_1"]) + (["allreduce_exposed"] if world > 1 else [])
-            if tr.side is None and world == 1:
+            shares = tr.overlap == "early"
+            names = ["mlp_fwd_0"] + ([] if shares else ["mlp_fwd_1"]) + (["allreduce_exposed"] if tr.exchange else [])
+            if tr.side is None and not tr.exchange:
                 names += [f"mlp_{k}_{i}" for i in (1, 0) for k in ("dx", "dw", "reduce")]
             tr.enable_probes(names)
             _, tr.dt_local_probed, tr.dt_probed = timed_window(tr, steps, warmup + steps)
@@ -600,7 +600,7 @@ def main():
 
     tr, dt, mse_f = run(args.precision, args.steps, args.warmup, probes=True)
     dist_info = distributed_fields(tr.dt_local, args.steps, tr.probe_ms().get("allreduce_exposed"), tr.grad_exchange,
-                                   dev) if world > 1 else None
+                                   dev) if parallel.is_dist() else None
     dt_probed = tr.dt_probed
     R, Pc, Pf = tr.R, tr.Pc, tr.Pf
     rays_total = R * world * args.steps

@@ -587,6 +587,121 @@ def gen_train_step_trained(out):
     out["train_step_trained"] = record_train_step(pcfg, "trained", pose, focal, img, n_rays, torch_seed=31)
 
 
+@contextmanager
+def replay_draws(log):
+    """Feed a Recorder's draws back, in order, to the same torch calls (cast to the dtype the caller asks for: the float64
+    re-run of a recorded fp32 trajectory consumes the same uniforms / normals / pixel ids)."""
+    names = ("multinomial", "rand_like", "randn_like", "rand")
+    orig = {n: getattr(torch, n) for n in names}
+    it = iter(list(log))
+
+    def make(name):
+        def g(*a, **k):
+            n_, v = next(it)
+            assert n_ == name, (n_, name)
+            if name in ("rand_like", "randn_like"):
+                return v.to(a[0].dtype)
+            if name == "rand":
+                return v.to(k.get("dtype") or torch.get_default_dtype())
+            return v.clone()
+        return g
+
+    for n in names:
+        setattr(torch, n, make(n))
+    try:
+        yield
+    finally:
+        for n, f in orig.items():
+            setattr(torch, n, f)
+
+
+TRAJ_HW, TRAJ_RAYS, TRAJ_STEPS = 32, 256, 20
+
+
+def gen_train_trajectory(out):
+    """Multi-step training parity: the reference's registry pipeline (lego.yml: 64 + 128 samples, density noise 0.2) with
+    the reference runner's optimizer and schedule (scripts/run.py:158-160: torch.optim.Adam over create_param_groups,
+    runners/utils.py:148-151; runners/apis.py:66-89 per iteration: create_lr_scheduler's decay, warmup_lr_scheduler while
+    passed_iter <= warmup_steps, zero_grad, objective.mean().backward(), optimizer.step()) for TRAJ_STEPS steps on
+    TRAJ_HW x TRAJ_HW views of the procedural scene (one view per step), TRAJ_RAYS rays per step, from the seeded Lego
+    weights (the reference's zero density bias). Every random draw of every step is recorded (pixel ids, stratified
+    jitter, both density-noise draws, refinement uniforms), with the per-step losses and learning rates, and the
+    parameters after the last step (whole tensors up to 4,096 elements, a fixed 256-entry sample of the larger ones).
+    The same trajectory is then re-run by the reference in float64 on the recorded draws: the exact algorithm's
+    parameters after the same steps, the yardstick both fp32 implementations are measured against."""
+    from yanerf.runners.utils import create_lr_scheduler, warmup_lr_scheduler
+    cfg = Config.fromfile(str(REF / "configs/nerf/lego.yml"))
+    runner = cfg.runner
+    pcfg = lego_pipeline_cfg(n_rays=TRAJ_RAYS, H=TRAJ_HW, W=TRAJ_HW)
+    focal = torch.tensor([0.5 * TRAJ_HW / np.tan(0.5 * 0.6911112070083618)], dtype=torch.float32)
+    views = [(-180.0 + 360.0 * k / TRAJ_STEPS, -30.0 + 10.0 * np.sin(k)) for k in range(TRAJ_STEPS)]
+    poses = [torch.from_numpy(synthetic_pose(th, ph, 4.0))[None] for th, ph in views]
+    images = [torch.from_numpy(np.ascontiguousarray(scene_view(th, ph, TRAJ_HW)))[None].float() for th, ph in views]
+    seeds = (61, 62)
+
+    def run(dtype, draws=None):
+        torch.set_default_dtype(dtype)
+        try:
+            pipe = PIPELINES.build(pcfg)
+            load_pipeline_weights(pipe, seeds)
+            pipe.to(dtype)
+            pipe.train()
+            opt = torch.optim.Adam([{"params": pipe.parameters(), "init_lr": runner.init_lr}], lr=runner.init_lr,
+                                   weight_decay=runner.weight_decay)
+            sched = create_lr_scheduler(opt, runner)
+            torch.manual_seed(70)
+            rec, logs, losses, lrs = Recorder(), [], [], []
+            for it in range(TRAJ_STEPS):
+                sched(iter=it)
+                if runner["warmup_steps"] > 0 and it <= runner["warmup_steps"]:
+                    warmup_lr_scheduler(opt, it, runner["warmup_steps"], runner["warmup_lr"])
+                lrs.append(opt.param_groups[0]["lr"])
+                opt.zero_grad()
+                kw = dict(poses=poses[it].to(dtype), focal_lengths=focal.to(dtype), image_rgb=images[it].to(dtype),
+                          evaluation_mode=EvaluationMode.TRAINING)
+                if draws is None:
+                    rec.log = []
+                    with rec.capture():
+                        preds = pipe(**kw)
+                    logs.append(list(rec.log))
+                else:
+                    with replay_draws(draws[it]):
+                        preds = pipe(**kw)
+                preds["objective"].mean().backward()
+                opt.step()
+                losses.append([float(preds["objective"].mean()), float(preds["loss_rgb_mse"].mean()),
+                               float(preds["loss_prev_stage_rgb_mse"].mean())])
+            return pipe, logs, np.array(losses, np.float64), np.array(lrs, np.float64)
+        finally:
+            torch.set_default_dtype(torch.float32)
+
+    pipe, logs, losses, lrs = run(torch.float32)
+    pipe64, _, losses64, _ = run(torch.float64, logs)
+    d = dict(seeds=np.array(seeds), n_rays=np.int64(TRAJ_RAYS), hw=np.int64(TRAJ_HW), steps=np.int64(TRAJ_STEPS),
+             focal=np32(focal), poses=np.concatenate([np32(p) for p in poses]),
+             images=np.concatenate([np32(i) for i in images]), losses=losses, losses_f64=losses64, lrs=lrs)
+    for it, log in enumerate(logs):
+        kinds = [n for n, _ in log]
+        assert kinds == ["multinomial", "rand_like", "randn_like", "rand", "randn_like"], kinds
+        d[f"pixel_ids:{it}"] = log[0][1].numpy().astype(np.int64)
+        d[f"jitter_u:{it}"] = np32(log[1][1])
+        d[f"noise_coarse:{it}"] = np32(log[2][1])
+        d[f"pdf_u:{it}"] = np32(log[3][1])
+        d[f"noise_fine:{it}"] = np32(log[4][1])
+    for i, (f, f64) in enumerate(zip(pipe.implicit_functions, pipe64.implicit_functions)):
+        p64 = dict(f64._fn.named_parameters())
+        for name, p in f._fn.named_parameters():
+            v, v64 = p.detach().numpy().astype(np.float32), p64[name].detach().numpy().astype(np.float64)
+            if v.size <= 4096:
+                d[f"param{i}:{name}"], d[f"param64_{i}:{name}"] = v, v64
+            else:
+                idx = np.random.Generator(np.random.PCG64(len(name) * 1000 + i)).choice(v.size, 256, replace=False)
+                d[f"paramidx{i}:{name}"] = idx.astype(np.int64)
+                d[f"param{i}:{name}"] = v.reshape(-1)[idx]
+                d[f"param64_{i}:{name}"] = v64.reshape(-1)[idx]
+    out["train_trajectory"] = d
+
+
 def gen_zero_outputer(out):
     """Known-answer (reference tests/test_pipeline.py:67-151): zero density -> rendered == bg exactly."""
     pcfg = lego_pipeline_cfg(n_rays=4)
@@ -821,7 +936,7 @@ def gen_iter_runner(out):
 GENERATORS = (gen_harmonic, gen_raysampler, gen_mlp, gen_raymarcher, gen_sample_pdf, gen_render_eval,
               gen_train_step, gen_zero_outputer, gen_init_checksums, gen_pipeline_state, gen_lr_schedule,
               gen_raysampler_masked, gen_iter_runner, gen_render_fern, gen_train_step_fern, gen_sensitivity,
-              gen_render_trained, gen_train_step_trained)
+              gen_render_trained, gen_train_step_trained, gen_train_trajectory)
 
 
 def main():

@@ -119,6 +119,14 @@ def split_gate(rgb, rgb_ref, z, z_ref, depth=None, depth_ref=None, *, fine_at=No
             np.abs(rgb - np.asarray(f_a, np.float64).reshape(R, -1)).max())
         if depth is not None:
             report["max_depth_err_all_vs_oracle_at_our_depths"] = float(np.abs(depth - np.asarray(d_a, np.float64)).max())
+    report["other_depth_rays"] = [int(i) for i in flip]
+    if sensitivity is not None:
+        report["outside_reference_sensitive_rays"] = [int(i) for i in np.nonzero(~same & ~sens)[0]]
+    dump = os.environ.get("YANERF_PARITY_DUMP")
+    if dump:  # the inputs of this gate, for offline analysis of the flipped rays (tools/, not a gate)
+        Path(dump).mkdir(parents=True, exist_ok=True)
+        np.savez(Path(dump) / (tag.replace(" ", "_") + ".npz"), z=z, z_ref=z_ref, rgb=rgb, rgb_ref=rgb_ref,
+                 w_coarse=np.asarray(coarse[2], np.float32) if coarse is not None else np.zeros(0, np.float32))
     print(f"split_gate {tag}: {report}")
     write_report("split_gate", tag, report)
     assert report["max_rgb_err_same_depths"] <= (strict if same_tol is None else same_tol), report

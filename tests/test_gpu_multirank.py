@@ -212,15 +212,18 @@ def _exchange_worker(rank, world, port, q, precision):
     g = torch.Generator().manual_seed(200 + rank)
     img = torch.rand(1, 800, 800, 3, generator=g).to("cuda:0")
     out = {}
-    for exch in ("bucketed", "single"):
+    # (bf16 defaults to the "early" schedule: the coarse backward and its bucket's all-reduce on the side stream beside
+    # the fine forward; "bucketed_serial" is the same exchange with the serial backward)
+    for name, exch, overlap in (("bucketed", "bucketed", None), ("single", "single", None),
+                                ("bucketed_serial", "bucketed", False)):
         tr = NeRFTrainer(cfg.pipeline, precision=precision, device="cuda:0", n_rays=256, runner_cfg=cfg.runner,
-                         seed=42, grad_exchange=exch)
+                         seed=42, grad_exchange=exch, overlap=overlap)
         for k in range(3):
             pose = torch.from_numpy(synthetic_pose(25.0 * k + 90.0 * rank, -30.0, 4.0)).float()[None].to("cuda:0")
             tr.step(pose, torch.tensor([1111.111], device="cuda:0"), img)
         torch.cuda.synchronize()
-        out[exch] = dict(params=tr.flat.data.detach().cpu().clone(), m=tr.exp_avg.detach().cpu().clone(),
-                         v=tr.exp_avg_sq.detach().cpu().clone())
+        out[name] = dict(params=tr.flat.data.detach().cpu().clone(), m=tr.exp_avg.detach().cpu().clone(),
+                         v=tr.exp_avg_sq.detach().cpu().clone(), overlap=tr.overlap)
         del tr
     q.put(_by_value((rank, out)))
     parallel.barrier()
@@ -231,13 +234,17 @@ def _exchange_worker(rank, world, port, q, precision):
 def test_bucketed_and_single_exchange_give_identical_parameters(precision):
     """configs[2]'s exchange (scripts/run.py:162-166 DDP semantics) in both of the trainer's schedules: after three
     steps on two ranks the bucketed (overlapped) and the single all-reduce give bit-identical parameters and Adam
-    moments, on both ranks, in fp32 and bf16 -- the bucketing changes when the sums run, not what they sum."""
+    moments, on both ranks, in fp32 and bf16 -- the bucketing changes when the sums run, not what they sum. bf16 runs
+    its default "early" schedule at world 2 (coarse backward + coarse bucket on the side stream beside the fine forward),
+    checked against the serial bucketed schedule as well."""
     res = _spawn(_exchange_worker, 2, extra=(precision,))
     (_, a), (_, b) = res
+    assert a["bucketed"]["overlap"] == ("early" if precision == "bf16" else False)
     for key in ("params", "m", "v"):
-        assert torch.equal(a["bucketed"][key], a["single"][key]), key
+        for other in ("single", "bucketed_serial"):
+            assert torch.equal(a["bucketed"][key], a[other][key]), (key, other)
+            assert torch.equal(b["bucketed"][key], b[other][key]), (key, other)
         assert torch.equal(a["bucketed"][key], b["bucketed"][key]), key
-        assert torch.equal(b["bucketed"][key], b["single"][key]), key
 
 
 def _rccl_world1_worker(rank, world, port, q):

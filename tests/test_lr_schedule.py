@@ -116,3 +116,12 @@ def test_lr_at_uses_restored_init_lr():
     for it in (0, 500, 1000, 1001, 5000, 123456):
         apply_schedule(opt, sched, r, it)
         assert lr_at(r, it, 1, init_lr=7e-4) == opt.param_groups[0]["lr"]
+
+
+def test_trajectory_golden_learning_rates(golden):
+    """The 20-step reference trajectory (train_trajectory.npz, make_golden.gen_train_trajectory) ran the lego.yml
+    schedule through the reference runner's own functions; the fused trainer's lr_at gives the same rate every step."""
+    g = golden("train_trajectory")
+    runner = _runner({})
+    got = np.array([lr_at(runner, k, 1) for k in range(int(g["steps"]))])
+    np.testing.assert_array_equal(got, g["lrs"])

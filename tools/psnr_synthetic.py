@@ -72,7 +72,8 @@ def run(data_dir: Path, precision: str, steps: int, dev, n_rays=4096, log=None, 
     res = {"precision": precision, "steps": steps, "rays_per_step": n_rays, "train_s": round(dt, 2),
            "rays_per_s": round(steps * n_rays / dt, 1), "test_psnr_fine": round(ev["loss_rgb_psnr"], 3),
            "test_psnr_coarse": round(ev["loss_prev_stage_rgb_psnr"], 3), "test_views": len(test),
-           "rays_before_far_plane": round(surface, 4), "seed": seed, "density_bias_init": density_bias}
+           "rays_before_far_plane": round(surface, 4), "seed": seed, "density_bias_init": density_bias,
+           "size": train.H}
     if log:
         print(json.dumps(res), file=log, flush=True)
     return res
@@ -86,13 +87,15 @@ def main():
     ap.add_argument("--data", default=None, help="existing scene dir (default: generate into a temp dir)")
     ap.add_argument("--save", default=None, help="write the last run's trained checkpoint to this file")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--rays", type=int, default=4096, help="rays per step")
     ap.add_argument("--density-bias", type=float, default=None, help="density-layer bias at init (reference: 0)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     with tempfile.TemporaryDirectory() as tmp:
         data = Path(a.data) if a.data else write_scene(Path(tmp) / "synthetic", a.size, 40, 8, device="cuda")
         out = {"scene": f"procedural blobs, {a.size}x{a.size}, 40 train / 8 test views, Lego config 64+128",
-               "runs": [run(data, p, a.steps, dev, log=sys.stderr, save=a.save, seed=a.seed, density_bias=a.density_bias)
+               "runs": [run(data, p, a.steps, dev, n_rays=a.rays, log=sys.stderr, save=a.save, seed=a.seed,
+                            density_bias=a.density_bias)
                         for p in a.precisions.split(",")]}
     print(json.dumps(out))
 

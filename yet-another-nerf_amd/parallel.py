@@ -26,7 +26,10 @@ def init_distributed(backend: Optional[str] = None) -> tuple:
     """Initialise the default process group from torchrun's env (MASTER_ADDR=127.0.0.1 on one node).
     Returns (rank, world_size, local_rank). world_size 1 -> no process group."""
     rank, world, local = env_rank_world()
-    if world > 1 and not dist.is_initialized():
+    # YANERF_PG_AT_WORLD1=1: a process group even at world size 1, so one card runs the N-rank step schedule with its
+    # collectives (bench.py's rehearsal of the exchange overlap against the plain N=1 line)
+    want = world > 1 or os.environ.get("YANERF_PG_AT_WORLD1") == "1"
+    if want and not dist.is_initialized():
         # YANERF_DIST_BACKEND=gloo: a rehearsal of the N-rank code path with several ranks on one card (RCCL needs one
         # card per rank); the measured runs use the default, RCCL
         backend = backend or os.environ.get("YANERF_DIST_BACKEND") or None
@@ -49,7 +52,8 @@ def device_index(local_rank: int) -> int:
 
 
 def is_dist() -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    """A process group is up (any size: a world-1 group over RCCL runs the N-rank code path, collectives included)."""
+    return dist.is_available() and dist.is_initialized()
 
 
 def allreduce_mean_(flat: torch.Tensor) -> torch.Tensor:

@@ -155,6 +155,10 @@ class NeRFTrainer:
             overlap = "early" if precision == "bf16" else False
         self.overlap = "both" if overlap is True else overlap
         self.side = torch.cuda.Stream(device=self.dev) if overlap else None
+        # the gradient exchange runs whenever a process group is up (at world 1 too: bench.py's YANERF_PG_AT_WORLD1
+        # rehearsal runs the N-rank schedule, collectives included, on one card)
+        self.exchange = parallel.is_dist()
+        self._h_early = None  # the coarse bucket's all-reduce, started on the side stream ("early")
         self.grad_exchange = grad_exchange or os.environ.get("YANERF_GRAD_EXCHANGE", "bucketed")
         if self.grad_exchange not in ("bucketed", "single"):
             raise ValueError(f"NeRFTrainer: grad_exchange {self.grad_exchange!r} (bucketed | single)")
@@ -371,30 +375,45 @@ class NeRFTrainer:
                                                      None, _p(noise), _p(ps.g_feats), None, None, R, P, C,
                                                      _p(ps.g_sigma), _p(ps.g_rgb), st), "yanerf_composite_backward")
             out["sq_coarse" if k == 0 else "sq_fine"] = ps.sq
-            if k == 0 and self.overlap == "early" and not self.kernel_probes and self.world == 1:
+            if k == 0 and self._early():
                 # the coarse pass's loss and gradients are complete here and nothing of the fine pass depends on them:
                 # its MLP backward (dX: MFMA-bound, dW: bandwidth-bound) runs on the side stream beside the refinement
-                # and the fine forward (MFMA-bound) instead of after it
+                # and the fine forward (MFMA-bound) instead of after it. Under data parallelism (bucketed exchange) the
+                # coarse bucket's all-reduce is started on the side stream right behind it, so it also runs beside the
+                # fine pass; only the fine bucket's all-reduce is exposed.
                 self.side.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(self.side):
                     self._mlp_backward(0, ctypes.c_void_p(self.side.cuda_stream), self.side)
-        if self.world > 1 and not self.kernel_probes and self.grad_exchange == "bucketed":
+                    if self.exchange and self.grad_exchange == "bucketed":
+                        self._h_early = parallel.allreduce_sum_async(self.flat.grad[:self.n_coarse])
+        early = self._early()
+        if self.exchange and not self.kernel_probes and self.grad_exchange == "bucketed":
             # Under data parallelism the gradient exchange is split in two buckets, one per model, overlapped with
-            # the backward: the coarse MLP's backward runs first, its 2.4 MB all-reduce starts on the
-            # collective stream and runs while the fine MLP's backward (the longer one) occupies the GPU; only the
-            # fine bucket's all-reduce is exposed before Adam. Per element the result is the same sum over ranks.
+            # the backward: the coarse MLP's backward runs first (or, "early", beside the fine forward on
+            # the side stream), its 2.4 MB all-reduce starts on the collective stream right behind it and runs while
+            # the fine MLP's backward (the longer one) occupies the GPU; only the fine bucket's all-reduce is exposed
+            # before Adam. Per element the result is the same sum over ranks.
             # Probe "allreduce_exposed": HIP events on the compute stream around the wait, i.e. the time the step
             # stalls on the exchange after its last backward kernel.
-            self._mlp_backward(0, st)
-            h = parallel.allreduce_sum_async(self.flat.grad[:self.n_coarse])
-            self._mlp_backward(1, st)
-            h2 = parallel.allreduce_sum_async(self.flat.grad[self.n_coarse:])
+            if early:
+                self._mlp_backward(1, st)
+                h2 = parallel.allreduce_sum_async(self.flat.grad[self.n_coarse:])
+                torch.cuda.current_stream().wait_stream(self.side)
+                h, self._h_early = self._h_early, None
+            else:
+                self._mlp_backward(0, st)
+                h = parallel.allreduce_sum_async(self.flat.grad[:self.n_coarse])
+                self._mlp_backward(1, st)
+                h2 = parallel.allreduce_sum_async(self.flat.grad[self.n_coarse:])
             self._probe("allreduce_exposed", lambda: (parallel.finish_allreduce(h), parallel.finish_allreduce(h2)))
             self.flat.grad.div_(self.world)
-        elif self.world > 1 and not self.kernel_probes:
+        elif self.exchange and not self.kernel_probes:
             # "single": both backwards, then one all-reduce of the whole flat gradient (all of it exposed)
             self._mlp_backward(1, st)
-            self._mlp_backward(0, st)
+            if early:
+                torch.cuda.current_stream().wait_stream(self.side)
+            else:
+                self._mlp_backward(0, st)
             self._probe("allreduce_exposed", lambda: parallel.allreduce_mean_(self.flat.grad))
         elif self.kernel_probes:
             # timing probe mode (bench.py's per-kernel roofline): every MLP backward kernel alone on the stream, in the
@@ -412,7 +431,7 @@ class NeRFTrainer:
             else:
                 self._mlp_backward(1, st)
                 self._mlp_backward(0, st)
-        elif self.overlap == "early":
+        elif early:
             self._mlp_backward(1, st)
             torch.cuda.current_stream().wait_stream(self.side)
         elif self.overlap == "split":
@@ -457,8 +476,8 @@ class NeRFTrainer:
         LLFF's per-image bound tensors, averaged as step() does), so a captured LLFF step follows each image's bounds;
         without them the range of the previous replay stays. Run at least one eager step first (the library's kernels
         load on first launch). Single rank only (a gloo exchange cannot be captured)."""
-        if self.world > 1:
-            raise NotImplementedError("NeRFTrainer.capture_step: single rank only")
+        if self.exchange:
+            raise NotImplementedError("NeRFTrainer.capture_step: single rank only (no process group)")
         if self.events is not None or self.kernel_probes:
             raise ValueError("NeRFTrainer.capture_step: disable timing probes first")
         self._check_inputs(pose, focal, image)
@@ -523,6 +542,11 @@ class NeRFTrainer:
         self.step_count += 1
         self._dstate_host = (self._dstate_host[0] + self._g_rng_delta, self._dstate_host[1] + 1)
         return self._g_out
+
+    def _early(self) -> bool:
+        """The "early" schedule: the coarse MLP backward on the side stream right after the coarse composite, beside
+        the refinement and the fine forward (kernel-probe steps serialise every backward kernel instead)."""
+        return self.overlap == "early" and not self.kernel_probes
 
     def _mlp_backward(self, k: int, st, stream=None, phase: int = 3):
         L = _C.lib()
@@ -632,6 +656,8 @@ class NeRFTrainer:
             rng_pre = self.rng.get_state()
             self.render(sp, sf, *key[:4], chunk=chunk)  # eager first: the evaluation buffers exist before the capture
             torch.cuda.synchronize(self.dev)
+            # the capture draws from the offsets an eager render() at this point would (the warm-up's draws are undone)
+            self.rng.set_state(rng_pre)
             rng0 = self.rng.get_state()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):

@@ -206,9 +206,13 @@ int yanerf_rgb_loss(const float* pred, const float* image, const float* xys, int
  * (nerf_pipeline.py:196-201, 307-324). values [B][R][C], xys [B][R][2] (integer-valued floats, pixel
  * x + W * y) -> out [B][H][W][C] = bg[c] (C floats; NULL = 0) everywhere, values at the rays' pixels.
  * Two rays on one pixel: one of them is written (torch's scatter_ leaves that order unspecified too).
+ * The pixel index is computed in float and truncated, as the reference's `.long()` of x + W * y (so images of 2^24
+ * pixels and more get the reference's own rounded indices). A ray whose index falls outside [0, H * W) -- where the
+ * reference's scatter_ raises -- is not written and sets *oob = 1 (a device int, may be NULL; never cleared here):
+ * the caller decides when to read it back (ops.scatter_rays raises like the reference).
  * ---------------------------------------------------------------------------------------------- */
 int yanerf_scatter_rays(const float* values, const float* xys, int64_t B, int64_t R, int64_t C, int64_t H,
-                        int64_t W, const float* bg, float* out, void* stream);
+                        int64_t W, const float* bg, float* out, int* oob, void* stream);
 
 /* Fused Adam step over a flat fp32 parameter buffer: torch.optim.Adam (run.py:158-160) with torch's arithmetic, one
  * element per lane. The scalars are doubles, as torch holds them in Python: bias corrections 1 - beta**step, the step

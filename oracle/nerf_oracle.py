@@ -29,15 +29,19 @@ f32 = np.float32
 # ============================================================================ helpers
 def torch_linspace(start: float, end: float, n: int) -> np.ndarray:
     """torch.linspace on CPU for float32: start + step*i on the first half, end - step*(n-1-i) on the second
-    (aten RangeFactoriesKernel linspace_kernel). Used at ray_sampler.py:285-291, renderers/utils.py:109."""
+    (aten RangeFactoriesKernel linspace_kernel), each a FUSED multiply-add in the compiled kernel (bit for bit against
+    torch.linspace on 449,515 values: tools/linspace_model.py). The fma is emulated in float64: step * i is exact there
+    (24-bit x <= 24-bit), so only the add rounds, then once more to float32 (a double rounding that never occurred in
+    the check). Used at ray_sampler.py:285-291, renderers/utils.py:109."""
     start, end = f32(start), f32(end)
     if n == 1:
         return np.array([start], dtype=f32)
     step = f32((end - start) / f32(n - 1))
     i = np.arange(n)
     half = n // 2
-    out = np.where(i < half, start + step * i.astype(f32), end - step * (n - 1 - i).astype(f32))
-    return out.astype(f32)
+    s64, i64 = np.float64(step), i.astype(np.float64)
+    out = np.where(i < half, s64 * i64 + np.float64(start), -s64 * (n - 1 - i64) + np.float64(end))
+    return out.astype(np.float32).astype(f32)
 
 
 def cumsum_acc64(x: np.ndarray, axis: int = -1) -> np.ndarray:

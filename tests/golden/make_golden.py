@@ -465,6 +465,156 @@ def gen_train_step_fern(out):
                                                              max_depth=far)
 
 
+# ----------------------------------------------------------------------------- the HIP kernels' summation order
+HIP_ORDER_INNER = 0  # how one v_mfma_f32_16x16x4_f32 combines its four products (profiles/r5_mfma_order.txt)
+
+
+def _hip_order_lib():
+    """tests/golden/mfma_order.c built with gcc (test infrastructure, this container only)."""
+    import ctypes
+    import subprocess
+    so = Path("/tmp/yanerf_mfma_order.so")
+    subprocess.run(["gcc", "-O2", "-fopenmp", "-shared", "-fPIC", "-o", str(so), str(HERE / "mfma_order.c"), "-lm"],
+                   check=True)
+    lib = ctypes.CDLL(str(so))
+    lib.hip_order_linear.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    return lib
+
+
+def _hip_linear(lib, x, w, b, bias_first):
+    """y = x W^T + b in the fp32 HIP GEMMs' order (mfma_order.c): the chain over 16-wide K-blocks, 4 MFMA k-steps each."""
+    K, N = w.shape[1], w.shape[0]
+    x2 = np.ascontiguousarray(x.detach().reshape(-1, K).numpy(), np.float32)
+    w2 = np.ascontiguousarray(w.detach().numpy(), np.float32)
+    b2 = None if b is None else np.ascontiguousarray(b.detach().numpy(), np.float32)
+    y = np.empty((x2.shape[0], N), np.float32)
+    lib.hip_order_linear(x2.ctypes.data, x2.shape[0], K, w2.ctypes.data, N, None if b2 is None else b2.ctypes.data,
+                         int(bias_first), HIP_ORDER_INNER, y.ctypes.data)
+    return torch.from_numpy(y).reshape(*x.shape[:-1], N)
+
+
+@contextmanager
+def hip_order_model(model, lib, pe="torch"):
+    """Evaluate one NeRFMLP (the reference's module) with every Linear in the HIP kernels' summation order: the trunk,
+    intermediate and colour layers accumulate from the bias, the density and colour-output heads (16-row MFMA tiles)
+    from zero with the bias added after (csrc/mlp.hip mlp_fwd_kernel); LinearWithRepeat is one K = 256 + 27 chain over
+    [Y, dirPE] as the kernel's K = 288 colour GEMM. pe="cr": the harmonic embedding's sin / cos correctly rounded
+    (float64, rounded once) instead of torch's vectorised ones (the fp32 kernels call the device libm sincosf)."""
+    from yanerf.pipelines.models.utils import HarmonicEmbedding, LinearWithRepeat
+    patched = []
+
+    def lin_fwd(mod):
+        head = mod.out_features <= 4
+        return lambda x: _hip_linear(lib, x, mod.weight, mod.bias, not head)
+
+    def lwr_fwd(mod):
+        def f(inp):
+            y, dpe = inp
+            full = torch.cat([y, dpe.unsqueeze(-2).expand(*y.shape[:-1], dpe.shape[-1])], dim=-1)
+            return _hip_linear(lib, full, mod.weight, mod.bias, True)
+        return f
+
+    def he_fwd(mod):
+        def f(x):
+            embed = (x[..., None] * mod._frequencies).view(*x.shape[:-1], -1)
+            e64 = embed.double()
+            sn, cs = e64.sin().float(), e64.cos().float()
+            return torch.cat((sn, cs, x) if mod.append_input else (sn, cs), dim=-1)
+        return f
+
+    for mod in model.modules():
+        if isinstance(mod, torch.nn.Linear):
+            mod.forward = lin_fwd(mod)
+        elif isinstance(mod, LinearWithRepeat):
+            mod.forward = lwr_fwd(mod)
+        elif isinstance(mod, HarmonicEmbedding) and pe == "cr":
+            mod.forward = he_fwd(mod)
+        else:
+            continue
+        patched.append(mod)
+    try:
+        yield
+    finally:
+        for mod in patched:
+            del mod.forward
+
+
+def hip_composite_weights(dens, lengths, dirs, background_opacity, density_bias):
+    """The emission-absorption weights as csrc/render.hip composite_kernel computes them (fp32, contraction off, the
+    capping exp correctly rounded, the running sum in double), for the reference's default options (exponential
+    capping, product weights, density ReLU, surface thickness 1): renderer.py EmissionAbsorptionRaymarcher.forward."""
+    f = np.float32
+    sig = dens[..., 0].astype(f)
+    z = lengths.astype(f)
+    d = dirs.astype(f)
+    dn = np.sqrt((d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2]).astype(f)
+    delta = np.concatenate([z[..., 1:] - z[..., :-1], np.full(z.shape[:-1] + (1,), background_opacity, f)], -1)
+    delta = (delta * dn[..., None]).astype(f)
+    v = (delta * (np.maximum(sig, f(0)) + f(density_bias))).astype(f)
+    exp_cr = lambda x: np.exp(x.astype(np.float64)).astype(f)  # noqa: E731
+    capped = (f(1) - exp_cr(-v)).astype(f)
+    cs = np.cumsum(v.astype(np.float64), axis=-1).astype(f)
+    op = (f(1) - exp_cr(-cs)).astype(f)
+    absorb = np.concatenate([np.ones(z.shape[:-1] + (1,), f), (f(1) - op[..., :-1]).astype(f)], -1)
+    return (capped * absorb).astype(f)
+
+
+@contextmanager
+def hip_raymarcher():
+    """The reference's raymarcher with its weights computed as the HIP composite kernel computes them
+    (hip_composite_weights); depths and features follow from those weights as in renderer.py:218-238."""
+    orig = EmissionAbsorptionRaymarcher.forward
+
+    def fwd(self, rays_densities, rays_features, aux, ray_lengths, ray_directions, density_noise_std=0.0,
+            bg_color=None):
+        assert density_noise_std == 0.0 and self.surface_thickness == 1 and self.density_relu
+        w = torch.from_numpy(hip_composite_weights(rays_densities.detach().numpy(), ray_lengths.detach().numpy(),
+                                                   ray_directions.detach().numpy(), float(self.background_opacity),
+                                                   float(self.background_density_bias)))
+        depths = (w * ray_lengths)[..., None].sum(dim=-2)
+        # opacity = the capped total (the last inclusive running sum)
+        deltas = torch.cat((ray_lengths[..., 1:] - ray_lengths[..., :-1],
+                            self.background_opacity * torch.ones_like(ray_lengths[..., :1])), dim=-1)
+        deltas = deltas * ray_directions[..., None, :].norm(p=2, dim=-1)
+        dens = torch.relu(rays_densities[..., 0]) + self.background_density_bias
+        opacities = self._capping_function(torch.cumsum(deltas * dens, dim=-1))[..., -1:]
+        if bg_color is None:
+            bg_color = self._bg_color.view(*([1] * len(rays_features.shape[:-2])), -1).expand(*rays_features.shape[:-2], -1)
+        features = (w[..., None] * rays_features).sum(dim=-2)
+        alpha = opacities if self.blend_output else 1
+        features = alpha * features + (1 - opacities) * bg_color
+        return features, depths, opacities, w, aux
+
+    EmissionAbsorptionRaymarcher.forward = fwd
+    try:
+        yield
+    finally:
+        EmissionAbsorptionRaymarcher.forward = orig
+
+
+@contextmanager
+def perturbed_refiner_weights(delta, rng):
+    """RayPointRefiner (renderers/utils.py:48-69) fed the coarse weights moved by delta x U(-1, 1) per element (clamped
+    at zero): coarse weights that differ from the reference's by the magnitude measured between an fp32 build and it."""
+    orig = RayPointRefiner.forward
+
+    def fwd(self, origins, directions, lengths, xys, ray_weights):
+        u = torch.from_numpy(rng.uniform(-1.0, 1.0, size=tuple(ray_weights.shape)).astype(np.float32))
+        return orig(self, origins, directions, lengths, xys, torch.clamp(ray_weights + delta * u, min=0.0))
+
+    RayPointRefiner.forward = fwd
+    try:
+        yield
+    finally:
+        RayPointRefiner.forward = orig
+
+
+# measured max |coarse weight (this build) - coarse weight (reference)| on the gated renders, fp32 and fp32x3 builds,
+# Lego 16 x 16, Fern 9 x 12, trained 25 x 25 (tools/dump_coarse_stage.py; profiles/r5_coarse_weight_deltas.json)
+WEIGHT_DELTA = 1.8e-7
+
+
 def gen_sensitivity(out):
     """How far the REFERENCE's own two-pass render moves under equally valid fp32 evaluations of its coarse stage: the
     Lego 16 x 16 evaluation render (render_eval_lego's config) and the Fern 9 x 12 renders (render_fern_*), each
@@ -534,6 +684,26 @@ def gen_sensitivity(out):
                 note(record_eval_render(pipe, pose, focal, H, W, **bounds))
             finally:
                 Fn.linear = flin
+        # (e) the coarse MLP in the fp32 HIP kernels' own summation order (the refined depths depend on it alone), with
+        # torch's harmonic embedding and with correctly rounded sin / cos; (f) the coarse weights moved by WEIGHT_DELTA
+        dz_e, dz_f = np.zeros(R), np.zeros(R)
+        lib = _hip_order_lib()
+        # the whole fp32 coarse stage as the HIP kernels evaluate it: correctly rounded embedding, the MFMA chain of
+        # every Linear, the composite's arithmetic (its coarse weights equal this build's bit for bit:
+        # tests/test_gpu_parity.py::test_hip_arithmetic_trial_reproduces_coarse_weights); then the reference's own
+        # RayPointRefiner / sample_pdf on them
+        with hip_order_model(coarse, lib, pe="cr"), hip_raymarcher():
+            r = record_eval_render(pipe, pose, focal, H, W, **bounds)
+        hip_w = r["coarse_weights"]
+        np.maximum(dz_e, np.abs(r["z_fine"].astype(np.float64) - base["z_fine"]).max(-1), out=dz_e)
+        with hip_order_model(coarse, lib, pe="torch"):  # the MFMA order alone, torch's embedding and raymarcher
+            r = record_eval_render(pipe, pose, focal, H, W, **bounds)
+        np.maximum(dz_e, np.abs(r["z_fine"].astype(np.float64) - base["z_fine"]).max(-1), out=dz_e)
+        for trial in range(8):
+            rng = np.random.Generator(np.random.PCG64(3000 + trial))
+            with perturbed_refiner_weights(WEIGHT_DELTA, rng):
+                r = record_eval_render(pipe, pose, focal, H, W, **bounds)
+            np.maximum(dz_f, np.abs(r["z_fine"].astype(np.float64) - base["z_fine"]).max(-1), out=dz_f)
         # (a) float64
         torch.set_default_dtype(torch.float64)
         pipe.double()
@@ -546,7 +716,9 @@ def gen_sensitivity(out):
         out[f"sensitivity_{name}"] = dict(
             trials=np.int64(20), max_z_move=dz.astype(np.float32), max_rgb_move=drgb.astype(np.float32),
             z_fine=base["z_fine"], fine_features=base["fine_features"], z_fine_f64=r64["z_fine"].astype(np.float64),
-            fine_features_f64=r64["fine_features"].astype(np.float64))
+            fine_features_f64=r64["fine_features"].astype(np.float64), max_z_move_hip_order=dz_e.astype(np.float32),
+            max_z_move_weights=dz_f.astype(np.float32), weight_delta=np.float32(WEIGHT_DELTA),
+            hip_arithmetic_coarse_weights=hip_w)
 
 
 # Parity at TRAINED weights: the Lego architecture trained 1,500 fused fp32 steps (tools/density_collapse_probe.py: seed

@@ -58,26 +58,46 @@ def oracle_fine_at(O, params_f, arch, origins, directions, raymarch_opts, bg=(0.
     return fine_at
 
 
+def sensitivity_trials(sens, z_tol=2e-5):
+    """Per trial family of make_golden.gen_sensitivity, the rays whose refined depths the REFERENCE itself moves by
+    more than z_tol under that equally valid fp32 evaluation of its coarse stage (boolean masks over the rays):
+    f64 = float64 end to end; ulp_reorder = exp one ulp off, coarse parameters one ulp off, Linear K-sums split;
+    hip_arithmetic = the coarse stage in the fp32 HIP kernels' own arithmetic (MFMA chain of every Linear, correctly
+    rounded embedding and capping exp, the composite's operation order; and the MFMA order alone); weights = the
+    coarse weights moved by the measured |this build - reference| magnitude (sens["weight_delta"])."""
+    out = {"f64": np.abs(np.asarray(sens["z_fine_f64"], np.float64) - sens["z_fine"]).max(-1) > z_tol,
+           "ulp_reorder": np.asarray(sens["max_z_move"]) > z_tol}
+    if "max_z_move_hip_order" in sens:
+        out["hip_arithmetic"] = np.asarray(sens["max_z_move_hip_order"]) > z_tol
+    if "max_z_move_weights" in sens:
+        out["weights"] = np.asarray(sens["max_z_move_weights"]) > z_tol
+    return out
+
+
 def reference_sensitive_rays(sens, z_tol=2e-5):
-    """The rays the REFERENCE itself moves by more than z_tol under equally valid fp32 evaluations of its coarse stage
-    (tests/golden/sensitivity_*.npz, make_golden.gen_sensitivity: float64 end to end, exp one ulp off, coarse
-    parameters one ulp off, Linear K-sums reordered): a boolean mask over the rays."""
-    f64 = np.abs(np.asarray(sens["z_fine_f64"], np.float64) - sens["z_fine"]).max(-1) > z_tol
-    return (np.asarray(sens["max_z_move"]) > z_tol) | f64
+    """The union of sensitivity_trials: every ray the reference itself moves under some equally valid fp32
+    evaluation of its coarse stage."""
+    m = None
+    for v in sensitivity_trials(sens, z_tol).values():
+        m = v if m is None else (m | v)
+    return m
 
 
 def split_gate(rgb, rgb_ref, z, z_ref, depth=None, depth_ref=None, *, fine_at=None, coarse=None, strict=1e-5,
                strict_depth=1e-4, z_tol=2e-5, tag="", sensitivity=None, same_tol=None, same_tol_depth=None,
-               all_vs_oracle=False):
+               all_vs_oracle=False, hip_exact=False):
     """coarse = (O, lengths [R,Pc], our coarse weights [R,Pc], n_fine): the oracle refinement of our coarse weights
     (deterministic, as the evaluation pass runs it) must equal z on every ray.
     same_tol / same_tol_depth: the bound on the rays whose refined depths agree with the reference's to z_tol (default
     strict / strict_depth). all_vs_oracle: every ray (not only those with other depths) is also held to strict /
     strict_depth against the oracle's fine stage at OUR refined depths -- for a sharp trained density, where depths
     equal to z_tol still move the colour by more than `strict` (the looser same_tol then bounds that effect).
-    sensitivity = the reference's own sensitivity golden of this render (reference_sensitive_rays): the number of rays
-    whose refined depths differ between this build and the reference must not exceed the number the reference itself
-    moves under ulp-level changes of its coarse stage; the rays outside that set are counted in the report."""
+    sensitivity = the reference's own sensitivity golden of this render (reference_sensitive_rays): every ray whose
+    refined depths differ between this build and the reference must lie in the set the reference itself moves under
+    equally valid fp32 evaluations of its coarse stage (set membership, asserted: none outside).
+    hip_exact (the fp32 mode, whose coarse weights the golden's hip-arithmetic trial reproduces bit for bit): the rays
+    with other depths must lie in that one trial's set -- the reference's own refinement of this build's coarse weights
+    moves exactly them."""
     R = len(z)
     rgb = np.asarray(rgb, np.float64).reshape(R, -1)
     rgb_ref = np.asarray(rgb_ref, np.float64).reshape(R, -1)
@@ -96,10 +116,16 @@ def split_gate(rgb, rgb_ref, z, z_ref, depth=None, depth_ref=None, *, fine_at=No
     if sensitivity is not None:
         sens = reference_sensitive_rays(sensitivity, z_tol)
         assert sens.shape == same.shape, (sens.shape, same.shape)
+        trials = sensitivity_trials(sensitivity, z_tol)
         report.update(reference_sensitive_rays=int(sens.sum()),
-                      reference_moved_by_f64=int((np.abs(np.asarray(sensitivity["z_fine_f64"]) - sensitivity["z_fine"])
-                                                  .max(-1) > z_tol).sum()),
-                      rays_with_other_depths_outside_reference_sensitive=int((~same & ~sens).sum()))
+                      reference_moved_by_f64=int(trials["f64"].sum()),
+                      reference_moved_by_trial={k: int(v.sum()) for k, v in trials.items()},
+                      other_depths_within_trial={k: int((~same & v).sum()) for k, v in trials.items()},
+                      rays_with_other_depths_outside_reference_sensitive=int((~same & ~sens).sum()),
+                      outside_without_weights_trial=int((~same & ~(trials["f64"] | trials["ulp_reorder"] | trials.get(
+                          "hip_arithmetic", np.zeros_like(same)))).sum()))
+        if hip_exact:
+            report["outside_hip_arithmetic_trial"] = int((~same & ~trials["hip_arithmetic"]).sum())
     if coarse is not None:
         O, zc, w_ours, n_fine = coarse
         zc = np.asarray(zc, np.float32).reshape(R, -1)
@@ -139,7 +165,10 @@ def split_gate(rgb, rgb_ref, z, z_ref, depth=None, depth_ref=None, *, fine_at=No
     if coarse is not None:
         assert report["max_depth_err_vs_oracle_refine_of_our_weights"] <= z_tol, report
     if sensitivity is not None:
-        assert report["rays_with_other_depths"] <= report["reference_sensitive_rays"], report
+        # set membership: the reference itself moves every one of these rays under some valid fp32 evaluation
+        assert report["rays_with_other_depths_outside_reference_sensitive"] == 0, report
+        if hip_exact:
+            assert report["outside_hip_arithmetic_trial"] == 0, report
     if flip.size:
         assert fine_at is not None, f"{flip.size} rays with other refined depths and no fine_at to account for them"
         assert coarse is not None, f"{flip.size} rays with other refined depths: pass `coarse` to close the loop"

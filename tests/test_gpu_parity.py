@@ -12,8 +12,8 @@ import pytest
 import torch
 
 from oracle import nerf_oracle as O
-from parity_gates import (golden_grad_items, golden_relu_masks, hip_relu_masks, loose_grad_gate, oracle_fine_at,
-                          split_gate, summarize_tie_budget, tie_budget_gate, write_report)
+from parity_gates import (TIE_REL, golden_grad_items, golden_relu_masks, hip_relu_masks, loose_grad_gate,
+                          oracle_fine_at, relu_ties, split_gate, summarize_tie_budget, tie_budget_gate, write_report)
 from weights import LEGO_ARCH, SMALL_ARCH, make_nerf_mlp_params
 
 pytestmark = pytest.mark.gpu
@@ -352,6 +352,10 @@ def test_render_eval_lego(pkg, golden, precision):
     close(n(pv.features).reshape(R, 3), g["coarse_features"].reshape(R, 3), 1e-5)
     close(n(pv.depths).reshape(R), g["coarse_depths"].reshape(R), 1e-4)
     close(n(pv.aux["weights"]).reshape(R, -1), g["coarse_weights"].reshape(R, -1), 1e-5)
+    np.testing.assert_array_equal(n(rb.lengths).reshape(R, -1), O.torch_linspace(2.0, 6.0, 64)[None].repeat(R, 0))
+    hipw = golden("sensitivity_lego")["hip_arithmetic_coarse_weights"].reshape(R, -1)
+    if precision == "fp32":  # bit for bit the reference's coarse stage in this build's fp32 arithmetic (make_golden)
+        np.testing.assert_array_equal(n(pv.aux["weights"]).reshape(R, -1), hipw)
     # fine stage driven by the reference's own coarse weights: strict
     ops = pkg["ops"]
     zf = ops.refine(rb.lengths.reshape(R, -1), t(g["coarse_weights"]).reshape(R, -1), 128, det=True)
@@ -368,7 +372,8 @@ def test_render_eval_lego(pkg, golden, precision):
                              o_r, d_r, O.RaymarchOpts(background_density_bias=1e-6))
     split_gate(n(preds["rendered_images"]), g["rendered_images"], z_gpu, n(zf), n(preds["rendered_depths"]),
                g["rendered_depths"], fine_at=fine_at, tag=f"render_eval_lego {precision}",
-               coarse=(O, n(rb.lengths), n(pv.aux["weights"]), 128), sensitivity=golden("sensitivity_lego"))
+               coarse=(O, n(rb.lengths), n(pv.aux["weights"]), 128), sensitivity=golden("sensitivity_lego"),
+               hip_exact=precision == "fp32")
     close(n(preds["loss_rgb_mse"]), g["loss_rgb_mse"], 2e-6)
 
 
@@ -451,6 +456,17 @@ def test_train_step_lego(pkg, golden, precision, depths):
     o_hip = O.train_step_grads(*args, *inputs, z_fine=z_ours, relu_masks=tuple(masks))
     o_ref = O.train_step_grads(*args, *inputs, z_fine=g["z_fine"],
                                relu_masks=(golden_relu_masks(g, 0), golden_relu_masks(g, 1)), abs_terms=True)
+    # the HIP forward's ReLU decisions differ from the reference's recorded ones (coarse; fine at the reference's
+    # depths) or from the oracle's own signs at our depths (fine, own depths) only at fp32 ties: the decisions the tie
+    # budget below is built from are pinned, as in the trainer's test (test_gpu_trainer.py)
+    ties = {}
+    for k, cache in ((0, o_hip["render"]["cache_c"]), (1, o_hip["render"]["cache_f"])):
+        if k == 0 or depths == "reference":
+            other = golden_relu_masks(g, k)
+        else:
+            other = dict(trunk=[zz > 0 for zz in cache.layer_pre], color=cache.c0_pre > 0)
+        ties[k] = relu_ties(masks[k], other, cache)
+        assert ties[k][1] <= TIE_REL, (k, ties[k])
     budget = {}
     loose = 0.0
     for i, name, v, ref, idx in golden_grad_items(g, [f._fn for f in pipe.implicit_functions]):
@@ -462,7 +478,8 @@ def test_train_step_lego(pkg, golden, precision, depths):
         budget[(i, name)] = tie_budget_gate(v, ref, oh, orf, f"{i}:{name}", abs_terms=ab)
         loose = max(loose, loose_grad_gate(v, ref, name, enforce=False))
     write_report("train_step", f"registry lego {precision} depths={depths}",
-                 dict(grad_worst_rel_l2_vs_reference=loose, tie_budget=summarize_tie_budget(budget)))
+                 dict(grad_worst_rel_l2_vs_reference=loose, relu_ties_coarse=ties[0][0], relu_ties_fine=ties[1][0],
+                      relu_tie_max_rel_preact=max(ties[0][1], ties[1][1]), tie_budget=summarize_tie_budget(budget)))
 
 
 def test_scatter_rays_bit_equal_to_reference_rasterization(pkg, golden):
@@ -506,6 +523,29 @@ def test_scatter_rays_roundtrip_and_background(pkg):
     hit.scatter_(1, (sub[..., 0] + W * sub[..., 1]).long().reshape(B, -1), True)
     assert torch.equal(out, ref)
     assert not torch.signbit(out.reshape(B, H * W)[~hit]).any()  # 0 + (-0) = +0 where no ray lands, as the reference
+
+
+def test_scatter_rays_reference_error_behaviour(pkg):
+    """scatter_rays_to_image's contract at its edges, as the reference's (pipelines/utils.py:299-323): a host [C]
+    bg_color (the reference's own test passes torch.Tensor([0, 0, 0]) on the CPU) fills the empty pixels; a bg_color
+    whose last dim is not C is ignored; a ray whose pixel index x + W * y lies outside the image raises, as torch's
+    scatter_ does (the kernel flags it on the device)."""
+    from yanerf_amd.pipelines.utils import scatter_rays_to_image
+    v = torch.rand(1, 4, 3, device=DEV)
+    xy = t([[[0, 0], [1, 0], [2, 1], [3, 1]]])
+    out = scatter_rays_to_image(v, xy, 2, 4, bg_color=torch.Tensor([0.25, 0.5, 0.75]))
+    ref = torch.zeros(1, 8, 3, device=DEV) + t([0.25, 0.5, 0.75])
+    ref.scatter_(1, (xy[..., 0] + 4 * xy[..., 1]).long()[..., None].expand(-1, -1, 3), v)
+    assert torch.equal(out.reshape(1, 8, 3), ref)
+    out = scatter_rays_to_image(v, xy, 2, 4, bg_color=torch.Tensor([0.5, 0.5]))  # wrong channel count: ignored
+    assert torch.equal(out.reshape(1, 8, 3)[:, [2, 3, 4, 5]], torch.zeros(1, 4, 3, device=DEV))
+    for bad in ([[[0, 0], [1, 0], [2, 5], [3, 1]]], [[[0, 0], [-3, 0], [2, 1], [3, 1]]]):
+        with pytest.raises(RuntimeError, match="outside"):
+            scatter_rays_to_image(v, t(bad), 2, 4)
+        with pytest.raises(RuntimeError):  # the reference's own operation on the same indices
+            xb = t(bad)
+            torch.zeros(1, 8, 3).scatter_(1, (xb[..., 0] + 4 * xb[..., 1]).long()[..., None].expand(-1, -1, 3).cpu(),
+                                          v.cpu())
 
 
 def test_zero_outputer_known_answer(pkg, golden):

@@ -451,6 +451,9 @@ def test_trainer_render_matches_reference_render(golden, case):
         # refined depths from our coarse weights vs from the reference's (the renderer's own intermediate)
         zc = t(O.sample_rays_eval(g["pose"], g["focal"], hw, hw, 2.0, 6.0, 64, H=H, W=W)[2].reshape(R, 64))
         rb_w = tr_coarse_weights(tr, g, H, W, hw)
+        if precision == "fp32":  # bit for bit the reference's coarse stage in this build's arithmetic (make_golden)
+            np.testing.assert_array_equal(n(rb_w), golden(f"sensitivity_{case}")["hip_arithmetic_coarse_weights"]
+                                          .reshape(R, -1))
         z_gpu = n(ops.refine(zc, rb_w, 128, det=True))
         z_ref = n(ops.refine(zc, t(g["coarse_weights"]).reshape(R, -1), 128, det=True))
         o_r, d_r, _, _ = O.sample_rays_eval(g["pose"], g["focal"], hw, hw, 2.0, 6.0, 64, H=H, W=W)
@@ -463,7 +466,8 @@ def test_trainer_render_matches_reference_render(golden, case):
         loose_same = {} if case == "lego" else dict(same_tol=1e-4, same_tol_depth=1e-3, all_vs_oracle=True)
         split_gate(n(f), g["fine_features"], z_gpu, z_ref, n(d), g["fine_depths"], fine_at=fine_at,
                    tag=f"render_eval {precision}" + ("" if case == "lego" else f" {case}"),
-                   coarse=(O, n(zc), n(rb_w), 128), sensitivity=golden(f"sensitivity_{case}"), **loose_same)
+                   coarse=(O, n(zc), n(rb_w), 128), sensitivity=golden(f"sensitivity_{case}"),
+                   hip_exact=precision == "fp32", **loose_same)
 
 
 def tr_coarse_weights(tr, g, H, W, hw=800):

@@ -1,0 +1,46 @@
+#!/usr/bin/env python
+"""BASELINE configs[3]'s single-GPU step (Fern 504x378, 64 + 128, 1024 rays, per-image bounds; bench.py extras
+fern_64_128_train) run for a few steps, for a rocprofv3 kernel trace of the small-batch step (tools/step_timeline.py).
+Development tool (GPU).   python tools/fern_steps.py [bf16|fp32] [steps] [eager|graph]"""
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "tests" / "golden")]
+import yanerf_boot  # noqa: E402
+from scene import synthetic_pose  # noqa: E402
+from yanerf_amd.train import NeRFTrainer  # noqa: E402
+from yanerf_amd.utils.config import Config  # noqa: E402
+
+prec = sys.argv[1] if len(sys.argv) > 1 else "bf16"
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 15
+mode = sys.argv[3] if len(sys.argv) > 3 else "eager"
+dev = torch.device("cuda:0")
+fcfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/fern.yml")).pipeline
+fcfg.renderer.n_pts_per_ray_fine_training = 128
+fcfg.renderer.n_pts_per_ray_fine_evaluation = 128
+fimg = torch.rand(1, 378, 504, 3, device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+ffocal = torch.tensor([407.56], device=dev)
+bounds = torch.tensor([[1.3, 5.9]])
+poses = torch.stack([torch.from_numpy(synthetic_pose(th, -30.0, 4.0)) for th in np.linspace(-180, 180, 40,
+                                                                                    endpoint=False)]).float().to(dev)
+tr = NeRFTrainer(fcfg, precision=prec, device=dev)
+kw = dict(near=bounds[:, :1], far=bounds[:, 1:])
+for i in range(3):
+    tr.step(poses[i:i + 1], ffocal, fimg, **kw)
+if mode == "graph":
+    tr.capture_step(poses[0:1], ffocal, fimg, **kw)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for i in range(steps):
+    if mode == "graph":
+        tr.replay_step(poses[(3 + i) % 40][None], ffocal, **kw)
+    else:
+        tr.step(poses[(3 + i) % 40][None], ffocal, fimg, **kw)
+torch.cuda.synchronize()
+dt = (time.perf_counter() - t0) / steps
+print(f"fern {prec} {mode}: {1e3 * dt:.4f} ms/step, {tr.R / dt:.1f} rays/s", flush=True)

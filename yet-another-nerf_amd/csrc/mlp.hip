@@ -1007,8 +1007,12 @@ __device__ __forceinline__ void harmonic_to_lds(typename Cfg<T>::lds_t* act, int
     float xi = x[0];
     xi = i == 1 ? x[1] : xi;
     xi = i == 2 ? x[2] : xi;
-    float sn, cs;
-    sincosf(xi * (float)(1 << f), &sn, &cs);  // the fp32 modes keep libm-accurate sin/cos
+    // the fp32 modes: correctly rounded sin / cos (evaluated in double, rounded once), so the embedding is a pure
+    // function of its fp32 argument that a CPU reproduces bit for bit (make_golden.hip_order_model); the device libm's
+    // sincosf differs from it in ~19 % of the Lego embedding values by an ulp. Its cost is < 1 % of the forward.
+    double sd, cd;
+    sincos((double)(xi * (float)(1 << f)), &sd, &cd);
+    const float sn = (float)sd, cs = (float)cd;
     lds_put1<T>(act, m, col0 + j, sn);
     lds_put1<T>(act, m, col0 + 3 * F + j, cs);
     if (sv) {

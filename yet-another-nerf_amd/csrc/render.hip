@@ -158,8 +158,12 @@ __device__ __forceinline__ float noise_at(const yanerf_raymarch_opts& o, const f
   return n * o.noise_std;
 }
 
-__device__ __forceinline__ float cap_fn(int kind, float x) { return kind == 0 ? 1.0f - expf(-x) : fminf(x, 1.0f); }
-__device__ __forceinline__ float cap_grad(int kind, float x) { return kind == 0 ? expf(-x) : (x <= 1.0f ? 1.0f : 0.0f); }
+// the capping function 1 - exp(-x) (renderer.py capping_function "exponential") with a correctly rounded exp (double,
+// rounded once): a pure function of its fp32 argument that a CPU reproduces bit for bit (make_golden's trial in the
+// HIP kernels' arithmetic); torch's vectorised expf is within an ulp of it
+__device__ __forceinline__ float exp_cr(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float cap_fn(int kind, float x) { return kind == 0 ? 1.0f - exp_cr(-x) : fminf(x, 1.0f); }
+__device__ __forceinline__ float cap_grad(int kind, float x) { return kind == 0 ? exp_cr(-x) : (x <= 1.0f ? 1.0f : 0.0f); }
 
 // the photometric loss of the fused training composite (MODE 2): rgb_loss_kernel's arithmetic on the ray's features
 struct CompositeLoss {
@@ -711,13 +715,17 @@ __global__ void scatter_fill_kernel(float* __restrict__ out, int64_t n, int64_t 
   }
 }
 __global__ void scatter_rays_kernel(const float* __restrict__ values, const float* __restrict__ xys, int64_t B,
-                                    int64_t R, int64_t C, int64_t H, int64_t W, float* __restrict__ out) {
+                                    int64_t R, int64_t C, int64_t H, int64_t W, float* __restrict__ out,
+                                    int* __restrict__ oob) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * R * C) return;
   const int64_t c = gid % C, br = gid / C, b = br / R;
   const float fi = xys[br * 2 + 0] + (float)W * xys[br * 2 + 1];
   const int64_t pix = (int64_t)fi;
-  if (pix < 0 || pix >= H * W) return;  // (the reference asserts nothing here; an out-of-image ray is dropped)
+  if (pix < 0 || pix >= H * W) {  // the reference's scatter_ raises on this index: flag it for the caller
+    if (oob) *oob = 1;            // (a plain store of the same value from every such lane)
+    return;
+  }
   out[(b * H * W + pix) * C + c] = values[gid];
 }
 
@@ -907,12 +915,10 @@ int yanerf_rgb_loss(const float* pred, const float* image, const float* xys, int
 }
 
 int yanerf_scatter_rays(const float* values, const float* xys, int64_t B, int64_t R, int64_t C, int64_t H, int64_t W,
-                        const float* bg, float* out, void* stream) {
+                        const float* bg, float* out, int* oob, void* stream) {
   YN_CHECK(B >= 0 && R >= 0 && C >= 1 && H >= 1 && W >= 1, "scatter_rays: bad sizes");
   YN_CHECK(out || B == 0, "scatter_rays: null output");
   YN_CHECK((values && xys) || B * R == 0, "scatter_rays: null pointer");
-  YN_CHECK(H * W < (1ll << 24), "scatter_rays: %lld pixels: the float pixel index is exact only below 2^24",
-           (long long)(H * W));
   const int64_t n = B * H * W * C;
   if (n == 0) return 0;
   hipLaunchKernelGGL(scatter_fill_kernel, dim3((unsigned)(((n + 3) / 4 + 255) / 256)), dim3(256), 0,
@@ -920,7 +926,7 @@ int yanerf_scatter_rays(const float* values, const float* xys, int64_t B, int64_
   YN_LAUNCH_CHECK("scatter_fill");
   if (B * R == 0) return 0;
   hipLaunchKernelGGL(scatter_rays_kernel, dim3((unsigned)((B * R * C + 255) / 256)), dim3(256), 0, as_stream(stream),
-                     values, xys, B, R, C, H, W, out);
+                     values, xys, B, R, C, H, W, out, oob);
   YN_LAUNCH_CHECK("scatter_rays");
   return 0;
 }

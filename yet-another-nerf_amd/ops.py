@@ -416,7 +416,14 @@ def rgb_loss(pred: torch.Tensor, image: torch.Tensor, xys: torch.Tensor, scale: 
 def scatter_rays(values: torch.Tensor, xys: torch.Tensor, image_height: int, image_width: int,
                  bg_color: Optional[torch.Tensor] = None) -> torch.Tensor:
     """scatter_rays_to_image (pipelines/utils.py:299-323) on the device: values [B, *spatial, C] at integer-valued
-    xys [B, *spatial, 2] onto a new [B, H, W, C] image filled with bg_color (when its last dim is C) or zeros."""
+    xys [B, *spatial, 2] onto a new [B, H, W, C] image filled with bg_color (when its last dim is C) or zeros. A host
+    bg_color (the reference's own test passes a CPU tensor) is moved to the device; one whose last dim is not C is
+    ignored, as the reference ignores it. A pixel index outside the image raises, as the reference's scatter_ does
+    (the kernel flags it on the device; this reads the flag back)."""
+    if bg_color is not None and bg_color.shape[-1] != values.shape[-1]:
+        bg_color = None
+    if bg_color is not None and not bg_color.is_cuda:
+        bg_color = bg_color.to(values.device)
     _dev(values, xys, bg_color)
     B, *ts, C = values.shape
     _, *gs, _ = xys.shape
@@ -430,8 +437,12 @@ def scatter_rays(values: torch.Tensor, xys: torch.Tensor, image_height: int, ima
                                       "passes None); only a [C] background is supported")
         bg = _f32c(bg_color.reshape(C))
     out = torch.empty(B, int(image_height), int(image_width), C, dtype=_F32, device=v.device)
+    oob = torch.zeros(1, dtype=torch.int32, device=v.device)
     _C.check(_C.lib().yanerf_scatter_rays(_p(v), _p(xy), B, v.shape[1], C, int(image_height), int(image_width),
-                                          _p(bg), _p(out), _stream()), "yanerf_scatter_rays")
+                                          _p(bg), _p(out), _p(oob), _stream()), "yanerf_scatter_rays")
+    if int(oob.item()):
+        raise RuntimeError(f"scatter_rays_to_image: a ray's pixel index x + W * y lies outside the {int(image_height)} "
+                           f"x {int(image_width)} image (torch's scatter_ raises on it: index out of bounds)")
     return out if values.dtype == _F32 else out.to(values.dtype)
 
 

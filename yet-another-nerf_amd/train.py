@@ -486,6 +486,7 @@ class NeRFTrainer:
         self._g_image = image.reshape(1, self.H, self.W, -1).contiguous()
         self._g_bounds = torch.empty(2, dtype=F32, device=self.dev)
         self._set_graph_bounds(near, far)
+        self._g_bounds_key = self._host_bounds_key(near, far)
         self._sync_step_state()
         rng0, step0, lr0, dstate0 = self.rng.get_state(), self.step_count, self.lr, self._dstate_host
         torch.cuda.synchronize(self.dev)
@@ -502,6 +503,18 @@ class NeRFTrainer:
         self.step_count, self.lr, self._dstate_host = step0, lr0, dstate0
         self.graph, self._g_out = g, out
         return out
+
+    @staticmethod
+    def _host_bounds_key(near, far):
+        """The averaged (near, far) of host-side bounds (floats or CPU tensors: LLFF's per-image bounds come from the
+        loader on the host), so a replay with the same values skips rewriting the graph's static bounds buffer (its
+        fill / reduce launches cost ~40 us on a 1 ms step); None when either is a device tensor or missing."""
+        out = []
+        for v in (near, far):
+            if v is None or (isinstance(v, torch.Tensor) and v.device.type != "cpu"):
+                return None
+            out.append(float(v.float().mean()) if isinstance(v, torch.Tensor) else float(v))
+        return tuple(out)
 
     def _set_graph_bounds(self, near, far):
         """Write the depth range of the next captured step into the static [near, far] buffer: None = the config's
@@ -526,8 +539,11 @@ class NeRFTrainer:
         if self.graph is None:
             raise RuntimeError("NeRFTrainer.replay_step: call capture_step first")
         if near is not None or far is not None:
-            cur = (self._g_bounds[0:1], self._g_bounds[1:2])
-            self._set_graph_bounds(cur[0].clone() if near is None else near, cur[1].clone() if far is None else far)
+            key = self._host_bounds_key(near, far)
+            if key is None or key != self._g_bounds_key:  # host bounds equal to the previous replay's: nothing to write
+                cur = (self._g_bounds[0:1], self._g_bounds[1:2])
+                self._set_graph_bounds(cur[0].clone() if near is None else near, cur[1].clone() if far is None else far)
+                self._g_bounds_key = key
         if pose is not None:
             self._g_pose.copy_(pose.reshape(1, -1, 4)[:, :3, :4])
         if focal is not None:

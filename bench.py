@@ -342,15 +342,19 @@ def extras(pcfg, cfg, dev, poses, focal, image, precision, others=()):
             tr.step(poses[(3 + i) % len(poses)][None], focal, image)
         torch.cuda.synchronize()
         eager_ms = 1e3 * (time.perf_counter() - t0) / nst
-        tr.capture_step(poses[0:1], focal, image)
-        tr.replay_step(poses[1:2], focal)
+        # GRAPH_STEPS consecutive steps per graph (capture_step(n_steps=...)): each replay copies its poses in one
+        # copy and launches one graph for all of them
+        K = GRAPH_STEPS
+        tr.capture_step(poses[0:K], focal, image, n_steps=K)
+        tr.replay_step(poses[K:2 * K], focal)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for i in range(nst):
-            tr.replay_step(poses[(3 + i) % len(poses)][None], focal)
+        for i in range(nst // K):
+            tr.replay_step(poses[(K * i) % len(poses):(K * i) % len(poses) + K], focal)
         torch.cuda.synchronize()
-        graph_ms = 1e3 * (time.perf_counter() - t0) / nst
+        graph_ms = 1e3 * (time.perf_counter() - t0) / (K * (nst // K))
         out["graph_step"][p] = {"eager_ms_per_step": round(eager_ms, 4), "graph_ms_per_step": round(graph_ms, 4),
+                                "graph_steps_per_launch": K,
                                 "graph_rays_per_s": round(tr.R / graph_ms * 1e3, 1),
                                 "step_mfma_frac_graph": round(train_flops_per_ray(tr.Pc, tr.Pf) * tr.R / (graph_ms * 1e-3)
                                                               / 1e12 / PEAK_TFLOPS[p], 4)}
@@ -380,16 +384,19 @@ def extras(pcfg, cfg, dev, poses, focal, image, precision, others=()):
         out["fern_64_128_train"][p] = {
             "rays_per_s": round(tr.R / dt, 1), "ms_per_step": round(1e3 * dt, 3),
             "step_mfma_frac": round(train_flops_per_ray(tr.Pc, tr.Pf) * tr.R / dt / 1e12 / PEAK_TFLOPS[p], 4)}
-        # the same steps replayed as a HIP graph (a 1024-ray step is short, so launch gaps weigh more); the captured
-        # step reads its per-image bounds from a static device buffer (replay_step(near=, far=))
-        tr.capture_step(poses[0:1], ffocal, fimg, near=bounds[:, :1], far=bounds[:, 1:])
-        tr.replay_step(poses[1:2], ffocal, near=bounds[:, :1], far=bounds[:, 1:])
+        # the same steps replayed as a HIP graph of GRAPH_STEPS steps per launch (a 1024-ray step is short, so the
+        # launch and input copies weigh more); the captured steps read their per-image bounds from a static device
+        # buffer (replay_step(near=, far=))
+        K = GRAPH_STEPS
+        tr.capture_step(poses[0:K], ffocal, fimg, near=bounds[:, :1], far=bounds[:, 1:], n_steps=K)
+        tr.replay_step(poses[K:2 * K], ffocal, near=bounds[:, :1], far=bounds[:, 1:])
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for i in range(nst):
-            tr.replay_step(poses[(3 + i) % len(poses)][None], ffocal, near=bounds[:, :1], far=bounds[:, 1:])
+        for i in range(nst // K):
+            tr.replay_step(poses[(K * i) % len(poses):(K * i) % len(poses) + K], ffocal, near=bounds[:, :1],
+                           far=bounds[:, 1:])
         torch.cuda.synchronize()
-        dtg = (time.perf_counter() - t0) / nst
+        dtg = (time.perf_counter() - t0) / (K * (nst // K))
         out["fern_64_128_train"][p].update(
             graph_rays_per_s=round(tr.R / dtg, 1), graph_ms_per_step=round(1e3 * dtg, 3),
             step_mfma_frac_graph=round(train_flops_per_ray(tr.Pc, tr.Pf) * tr.R / dtg / 1e12 / PEAK_TFLOPS[p], 4))
@@ -514,6 +521,7 @@ def dist_selftest(steps: int) -> None:
 DTYPES = {"fp32": "f32", "fp32x3": "f32 (3xbf16 split MFMA)",
           "bf16": "bf16 + fp8 (bf16 MFMA forward / dX; e4m3 saved activations and gradient rows; dW on the fp8 MFMA)"}
 LEGO_TRAIN_IMAGES = 100  # nerf_synthetic Lego's train split (the loader length scripts/run.py:243-271 converts with)
+GRAPH_STEPS = 4  # training steps captured per HIP graph in the graph legs (NeRFTrainer.capture_step(n_steps=...))
 
 
 def progress(msg: str) -> None:

@@ -610,6 +610,38 @@ def test_backward_schedules_give_identical_steps(precision):
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_multi_step_graph_equals_eager_steps(precision):
+    """capture_step(n_steps=3): three consecutive training steps in ONE graph, each reading its own pose / focal /
+    depth-range row; two replays run steps 1-6 bit for bit as six eager steps (losses of each replay's last step,
+    parameters, Adam moments, the Philox stream and the learning rate), with per-step LLFF-style bounds."""
+    from scene import synthetic_pose
+    from yanerf_amd.train import NeRFTrainer
+    cfg = lego_cfg()
+    trs = [NeRFTrainer(cfg.pipeline, precision=precision, device=DEV, n_rays=512, runner_cfg=cfg.runner, seed=6)
+           for _ in range(2)]
+    img = torch.rand(1, 800, 800, 3, device=DEV, generator=torch.Generator(device=DEV).manual_seed(7))
+    poses = torch.stack([torch.from_numpy(synthetic_pose(20.0 * k, -30.0, 4.0)).float() for k in range(7)]).to(DEV)
+    focal = torch.tensor([1111.111], device=DEV)
+    near = torch.tensor([[2.0], [2.1], [1.9], [2.2], [2.0], [2.05], [1.95]])
+    far = torch.tensor([[6.0], [5.9], [6.1], [5.8], [6.0], [6.2], [5.95]])
+    eager, graph = trs
+    losses = []
+    for k in range(7):
+        out = eager.step(poses[k:k + 1], focal, img, near=near[k:k + 1], far=far[k:k + 1])
+        losses.append((out["sq_coarse"].clone(), out["sq_fine"].clone()))
+    graph.step(poses[0:1], focal, img, near=near[0:1], far=far[0:1])
+    graph.capture_step(poses[1:4], focal, img, near=near[1:4], far=far[1:4], n_steps=3)
+    for r, k0 in enumerate((1, 4)):
+        out = graph.replay_step(poses[k0:k0 + 3], focal, near=near[k0:k0 + 3], far=far[k0:k0 + 3])
+        torch.cuda.synchronize()
+        assert torch.equal(out["sq_coarse"], losses[k0 + 2][0]) and torch.equal(out["sq_fine"], losses[k0 + 2][1]), r
+    assert graph.step_count == eager.step_count == 7 and graph.lr == eager.lr
+    assert graph.rng.get_state() == eager.rng.get_state()
+    for a, b in ((eager.flat.data, graph.flat.data), (eager.exp_avg, graph.exp_avg), (eager.exp_avg_sq, graph.exp_avg_sq)):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_graph_render_equals_eager_render(precision):
     """NeRFTrainer.render_graph: the whole chunked evaluation render of an image captured as one HIP graph and
     replayed per camera (one graph launch per image) gives bit for bit render()'s images, for the captured camera and

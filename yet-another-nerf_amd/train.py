@@ -200,16 +200,16 @@ class NeRFTrainer:
         self._pinned_keep = self._pinned_keep[-7:] + [p]
         return p
 
-    def _sync_step_state(self) -> int:
+    def _sync_step_state(self, span: int = 1) -> int:
         """Make the device step state describe the next step (Philox base = the host stream's offset, Adam table row =
-        this step's), uploading the schedule table when the step leaves it or its inputs changed. Returns the host
-        Philox offset at the start of the step. In steady state nothing is uploaded (no host sync)."""
+        this step's), uploading the schedule table when the next `span` steps leave it or its inputs changed. Returns
+        the host Philox offset at the start of the step. In steady state nothing is uploaded (no host sync)."""
         seed, off = self.rng.get_state()
         s = self.step_count
         key = (None if self.runner_cfg is not None else float(self.lr), float(self.init_lr), tuple(self.betas))
         if self._tab.shape[0] != self.TAB_STEPS:
             self._tab, self._tab_key = torch.empty(self.TAB_STEPS, 2, dtype=F32, device=self.dev), None
-        if self._tab_key != key or not (self._tab_base <= s < self._tab_base + self.TAB_STEPS):
+        if self._tab_key != key or not (self._tab_base <= s and s + span <= self._tab_base + self.TAB_STEPS):
             L = _C.lib()
             host = torch.empty(self.TAB_STEPS, 2, dtype=F32)
             base = host.data_ptr()
@@ -466,97 +466,122 @@ class NeRFTrainer:
         return out
 
     # --------------------------------------------------------------------------------------- hipGraph
-    def capture_step(self, pose: torch.Tensor, focal: torch.Tensor, image: torch.Tensor, near=None, far=None):
-        """Capture one training step as a HIP graph (torch.cuda.CUDAGraph over the same launch sequence as step()).
-        Every per-step scalar lives on the device (Philox base, Adam table row; _sync_step_state), so replay_step()
-        runs step after step with each step's own draws, learning rate and bias corrections, bit for bit the steps
-        step() would run. pose / focal are copied into static buffers at each replay; the image buffer is captured by
-        reference (replay_step(image=...) copies a different one into it). The depth range lives in a static device
-        buffer [near, far] that the captured ray generation reads: replay_step(near=, far=) rewrites it (floats or
-        LLFF's per-image bound tensors, averaged as step() does), so a captured LLFF step follows each image's bounds;
-        without them the range of the previous replay stays. Run at least one eager step first (the library's kernels
-        load on first launch). Single rank only (a gloo exchange cannot be captured)."""
+    def capture_step(self, pose: torch.Tensor, focal: torch.Tensor, image: torch.Tensor, near=None, far=None,
+                     n_steps: int = 1):
+        """Capture `n_steps` consecutive training steps as ONE HIP graph (torch.cuda.CUDAGraph over the launch sequence
+        of step(), n_steps times). Every per-step scalar lives on the device (Philox base, Adam table row;
+        _sync_step_state), so replay_step() runs the captured steps with each step's own draws, learning rate and bias
+        corrections, bit for bit the steps step() would run. Step k of a replay reads pose / focal / depth range from
+        row k of static buffers: pose [n_steps, 3|4, 4] and focal [n_steps] (or one row, used for every step) are
+        copied into them at each replay; the image buffer is captured by reference (replay_step(image=...) copies a
+        different one into it). near / far: floats, or LLFF's per-image bound tensors (averaged as step() does; one
+        value for all steps, or n_steps rows); without them the range of the previous replay stays. Several steps per
+        graph amortise the graph launch and the input copies over the steps (a 1,024-ray step is ~1 ms). Run at least
+        one eager step first (the library's kernels load on first launch). Single rank only (a gloo exchange cannot be
+        captured)."""
         if self.exchange:
             raise NotImplementedError("NeRFTrainer.capture_step: single rank only (no process group)")
         if self.events is not None or self.kernel_probes:
             raise ValueError("NeRFTrainer.capture_step: disable timing probes first")
-        self._check_inputs(pose, focal, image)
-        self._g_pose = pose.reshape(1, -1, 4)[:, :3, :4].contiguous().clone()
-        self._g_focal = focal.reshape(1).contiguous().clone()
+        K = int(n_steps)
+        if not 1 <= K <= self.TAB_STEPS:
+            raise ValueError(f"NeRFTrainer.capture_step: n_steps {n_steps} out of [1, {self.TAB_STEPS}]")
+        poses = self._step_rows(pose.reshape(-1, pose.shape[-2], 4)[:, :3, :4], K, "pose")
+        self._check_inputs(poses[0:1], focal.reshape(-1)[0:1], image)
+        self._g_K = K
+        self._g_pose = poses.contiguous().clone()
+        self._g_focal = self._step_rows(focal.reshape(-1), K, "focal").contiguous().clone()
         self._g_image = image.reshape(1, self.H, self.W, -1).contiguous()
-        self._g_bounds = torch.empty(2, dtype=F32, device=self.dev)
+        self._g_bounds = torch.empty(K, 2, dtype=F32, device=self.dev)
         self._set_graph_bounds(near, far)
         self._g_bounds_key = self._host_bounds_key(near, far)
-        self._sync_step_state()
+        self._sync_step_state(span=K)
         rng0, step0, lr0, dstate0 = self.rng.get_state(), self.step_count, self.lr, self._dstate_host
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
         self._capturing = True
         try:
             with torch.cuda.graph(g):
-                out = self.step(self._g_pose, self._g_focal, self._g_image, self._g_bounds[0:1], self._g_bounds[1:2])
+                for k in range(K):
+                    out = self.step(self._g_pose[k:k + 1], self._g_focal[k:k + 1], self._g_image,
+                                    self._g_bounds[k, 0:1], self._g_bounds[k, 1:2])
         finally:
             self._capturing = False
-        # the capture ran nothing: undo the captured step's host bookkeeping; each replay re-applies it
+        # the capture ran nothing: undo the captured steps' host bookkeeping; each replay re-applies it
         self._g_rng_delta = self.rng.get_state()[1] - rng0[1]
         self.rng.set_state(rng0)
         self.step_count, self.lr, self._dstate_host = step0, lr0, dstate0
         self.graph, self._g_out = g, out
         return out
 
+    def _step_rows(self, x: torch.Tensor, K: int, name: str) -> torch.Tensor:
+        """x with K rows along dim 0 (one row is repeated for every captured step)."""
+        if x.shape[0] == K:
+            return x
+        if x.shape[0] == 1:
+            return x.expand(K, *x.shape[1:])
+        raise ValueError(f"NeRFTrainer: {name} has {x.shape[0]} rows for {K} captured steps")
+
     @staticmethod
     def _host_bounds_key(near, far):
-        """The averaged (near, far) of host-side bounds (floats or CPU tensors: LLFF's per-image bounds come from the
+        """The (near, far) rows of host-side bounds (floats or CPU tensors: LLFF's per-image bounds come from the
         loader on the host), so a replay with the same values skips rewriting the graph's static bounds buffer (its
-        fill / reduce launches cost ~40 us on a 1 ms step); None when either is a device tensor or missing."""
+        fill launches cost ~10 us each on a ~1 ms step); None when either is a device tensor or missing."""
         out = []
         for v in (near, far):
             if v is None or (isinstance(v, torch.Tensor) and v.device.type != "cpu"):
                 return None
-            out.append(float(v.float().mean()) if isinstance(v, torch.Tensor) else float(v))
+            out.append(tuple(v.float().reshape(v.shape[0] if v.dim() > 1 else 1, -1).mean(-1).tolist())
+                       if isinstance(v, torch.Tensor) else float(v))
         return tuple(out)
 
     def _set_graph_bounds(self, near, far):
-        """Write the depth range of the next captured step into the static [near, far] buffer: None = the config's
-        value; floats; tensors averaged (ray_sampler.py:280-283) -- host tensors on the host, device tensors on the
-        device (no host sync)."""
+        """Write the depth range of the captured steps into the static [K, 2] buffer: None = the config's value;
+        floats; tensors averaged per step (ray_sampler.py:280-283; [K, ...] rows, or one value for every step) -- host
+        tensors on the host, device tensors on the device (no host sync)."""
+        K = self._g_bounds.shape[0]
         for i, (v, dflt) in enumerate(((near, self.near), (far, self.far))):
             v = dflt if v is None else v
             if isinstance(v, torch.Tensor):
-                v = v.float().mean()
+                v = v.float().reshape(v.shape[0] if v.dim() > 1 else 1, -1).mean(-1)
+                if v.numel() not in (1, K):
+                    raise ValueError(f"NeRFTrainer: {v.numel()} depth bounds for {K} captured steps")
                 if v.device.type == "cpu":
-                    v = float(v)
+                    v = v.tolist()
             if isinstance(v, torch.Tensor):
-                self._g_bounds[i:i + 1].copy_(v.reshape(1))
+                self._g_bounds[:, i].copy_(v.expand(K))
+            elif isinstance(v, list) and len(v) == K and K > 1:
+                self._g_bounds[:, i].copy_(torch.tensor(v, dtype=F32), non_blocking=False)
             else:
-                self._g_bounds[i:i + 1].fill_(float(v))
+                self._g_bounds[:, i].fill_(float(v[0] if isinstance(v, list) else v))
 
     def replay_step(self, pose: Optional[torch.Tensor] = None, focal: Optional[torch.Tensor] = None,
                     image: Optional[torch.Tensor] = None, near=None, far=None) -> Dict[str, torch.Tensor]:
-        """One training step by replaying the captured graph (capture_step), on `pose` / `focal` (copied into the
-        static buffers; default: the previous ones), the captured image buffer and the depth range near / far
-        (default: the previous replay's)."""
+        """The captured step(s) by replaying the graph (capture_step): n_steps training steps on `pose` / `focal`
+        (n_steps rows or one; copied into the static buffers; default: the previous ones), the captured image buffer
+        and the depth range near / far (default: the previous replay's). Returns the last step's outputs."""
         if self.graph is None:
             raise RuntimeError("NeRFTrainer.replay_step: call capture_step first")
+        K = self._g_K
         if near is not None or far is not None:
             key = self._host_bounds_key(near, far)
             if key is None or key != self._g_bounds_key:  # host bounds equal to the previous replay's: nothing to write
-                cur = (self._g_bounds[0:1], self._g_bounds[1:2])
-                self._set_graph_bounds(cur[0].clone() if near is None else near, cur[1].clone() if far is None else far)
+                cur = (self._g_bounds[:, 0].clone(), self._g_bounds[:, 1].clone())
+                self._set_graph_bounds(cur[0] if near is None else near, cur[1] if far is None else far)
                 self._g_bounds_key = key
         if pose is not None:
-            self._g_pose.copy_(pose.reshape(1, -1, 4)[:, :3, :4])
+            self._g_pose.copy_(self._step_rows(pose.reshape(-1, pose.shape[-2], 4)[:, :3, :4], K, "pose"))
         if focal is not None:
-            self._g_focal.copy_(focal.reshape(1))
+            self._g_focal.copy_(self._step_rows(focal.reshape(-1), K, "focal"))
         if image is not None and image.data_ptr() != self._g_image.data_ptr():
             self._g_image.copy_(image.reshape(self._g_image.shape))
-        self._sync_step_state()  # no-op in steady state; uploads the next schedule rows every TAB_STEPS steps
-        self.lr = self.current_lr()
+        self._sync_step_state(span=K)  # no-op in steady state; uploads the next schedule rows every TAB_STEPS steps
         self.graph.replay()
         seed, off = self.rng.get_state()
         self.rng.set_state((seed, off + self._g_rng_delta))
-        self.step_count += 1
-        self._dstate_host = (self._dstate_host[0] + self._g_rng_delta, self._dstate_host[1] + 1)
+        self.step_count += K
+        self.lr = self._lr_of_step(self.step_count - 1)
+        self._dstate_host = (self._dstate_host[0] + self._g_rng_delta, self._dstate_host[1] + K)
         return self._g_out
 
     def _early(self) -> bool:

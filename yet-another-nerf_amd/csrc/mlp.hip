@@ -2208,12 +2208,15 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
       adv[i] = 0;
     }
   }
+  // the operand stream is read once per launch (every split its own points, BK = 256: each gradient row in one
+  // k-tile), so the LDS-DMA loads go non-temporal (aux 2: MI355X_MICROARCH.md nt-weights): bf16 fine dW 0.79 -> 0.755 ms
+  // (microbench, two interleaved rounds, gradients bitwise equal: profiles/r5_ab_bf16_dw_nt.jsonl)
   auto issue = [&](int64_t st) {
     char* dst = smem + ((int)st % PM_STAGES) * PM_STAGE_BYTES;  // 32-bit modulo (the ring depth need not be 2^k)
 #pragma unroll
     for (int i = 0; i < PW; ++i)
       __builtin_amdgcn_global_load_lds(src[i] + st * adv[i],
-                                       (__attribute__((address_space(3))) void*)(dst + (8 * i + wave) * 1024), 16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)(dst + (8 * i + wave) * 1024), 16, 0, 2);
   };
   float* const scl = (float*)(smem + PM_STAGES * PM_STAGE_BYTES);
   const int64_t t0 = st_lo / SPT;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """BASELINE configs[3]'s single-GPU step (Fern 504x378, 64 + 128, 1024 rays, per-image bounds; bench.py extras
 fern_64_128_train) run for a few steps, for a rocprofv3 kernel trace of the small-batch step (tools/step_timeline.py).
-Development tool (GPU).   python tools/fern_steps.py [bf16|fp32] [steps] [eager|graph] [steps per graph] [default|serial|early|both|split]"""
+Development tool (GPU).   python tools/fern_steps.py [bf16|fp32] [steps] [eager|graph] [steps per graph] [default|serial|early|both|split] [hiprio]"""
 import sys
 import time
 from pathlib import Path
@@ -28,6 +28,8 @@ ffocal = torch.tensor([407.56], device=dev)
 bounds = torch.tensor([[1.3, 5.9]])
 poses = torch.stack([torch.from_numpy(synthetic_pose(th, -30.0, 4.0)) for th in np.linspace(-180, 180, 40,
                                                                                     endpoint=False)]).float().to(dev)
+if len(sys.argv) > 6 and sys.argv[6] == "hiprio":  # the step's main stream at high priority, the side stream at default
+    torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
 ov = sys.argv[5] if len(sys.argv) > 5 else "default"
 ov = {"default": None, "serial": False}.get(ov, ov)
 tr = NeRFTrainer(fcfg, precision=prec, device=dev, overlap=ov)
@@ -49,5 +51,6 @@ for i in range(steps // K if mode == "graph" else steps):
         n_done += 1
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / n_done
-print(f"fern {prec} {mode} K={K if mode == 'graph' else 1} overlap={tr.overlap}: {1e3 * dt:.4f} ms/step, "
+print(f"fern {prec} {mode} K={K if mode == 'graph' else 1} overlap={tr.overlap} "
+      f"main-priority={torch.cuda.current_stream().priority}: {1e3 * dt:.4f} ms/step, "
       f"{tr.R / dt:.1f} rays/s", flush=True)

@@ -99,6 +99,10 @@ int64_t yanerf_mlp_packed_bytes(const yanerf_mlp_desc* d, int precision);
  * and head sections. Call after every optimizer step (cost: one pass over 1.2 M parameters). */
 int yanerf_mlp_pack(const yanerf_mlp_desc* d, int precision, const float* const* params, void* packed,
                     void* stream);
+/* yanerf_mlp_pack for several MLPs of one precision in ONE launch (the trainer's coarse and fine models every step):
+ * d[m], params[m], packed[m] as yanerf_mlp_pack's for model m. Same bytes as n_models separate calls. */
+int yanerf_mlp_pack_multi(int n_models, const yanerf_mlp_desc* d, int precision, const float* const* const* params,
+                          void* const* packed, void* stream);
 /* Bytes of the per-call activation store kept from forward to backward for N points (0 for inference). */
 int64_t yanerf_mlp_saved_bytes(const yanerf_mlp_desc* d, int precision, int64_t n_points);
 /* Bytes of the backward workspace for N points (gradient rows + split-K partial slabs). */

@@ -407,6 +407,36 @@ def test_adam_matches_torch_adam(wd):
             assert torch.equal(a, b), (name, step, eq)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp32x3"])
+def test_pack_multi_equals_separate_packs(precision):
+    """yanerf_mlp_pack_multi (both of the trainer's models in one launch) writes exactly the bytes of one
+    yanerf_mlp_pack per model -- two Lego-size MLPs, and a pair of different architectures (8 layers with a skip, and
+    4 layers without, 128 hidden) so the jobs of unlike layouts share the launch."""
+    import ctypes
+    from yanerf_amd import _C, ops
+    from yanerf_amd.pipelines.models import MODELS
+    L = _C.lib()
+    for archs in ((dict(), dict()), (dict(), dict(n_layers=4, input_skips=[], n_hidden_neurons_xyz=128))):
+        models = []
+        for i, kw in enumerate(archs):
+            torch.manual_seed(10 + i)
+            models.append(MODELS.build(dict(type="NeRFMLP", precision=precision, **kw)).to(DEV))
+        specs = [m.spec() for m in models]
+        params = [[p.detach().contiguous() for p in m.hip_params()] for m in models]
+        nbytes = [L.yanerf_mlp_packed_bytes(ctypes.byref(s.desc()), s.precision) for s in specs]
+        ref = [ops.mlp_pack(s, ps, out=torch.full((nb,), 0xAB, dtype=torch.uint8, device=DEV))
+               for s, ps, nb in zip(specs, params, nbytes)]
+        outs = [torch.full_like(r, 0xAB) for r in ref]  # the same bytes written, the same left alone
+        tables = [_C.ptr_array([p.data_ptr() for p in ps]) for ps in params]
+        descs = (_C.MlpDesc * 2)(*[s.desc() for s in specs])
+        _C.check(L.yanerf_mlp_pack_multi(2, descs, specs[0].precision,
+                                         _C.ptr_array([ctypes.addressof(t) for t in tables]),
+                                         _C.ptr_array([o.data_ptr() for o in outs]), ops._stream()), "pack_multi")
+        torch.cuda.synchronize()
+        for r, o in zip(ref, outs):
+            assert torch.equal(r, o), archs
+
+
 def test_rgb_loss_matches_sample_grid_mse():
     """yanerf_rgb_loss (the fused step's loss) against the reference formulation: sample_grid gathers the target at
     the integer xys (pipelines/utils.py:272-296), per-ray squared error, and autograd of scale * sum((pred - gt)^2)."""

@@ -21,7 +21,8 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, r.get("Queue_Id", "?"),
                          int(r["Grid_Size_X"])))
     rows.sort()
-    ends = [i for i, r in enumerate(rows) if r[2].startswith(("adam_kernel", "adam_table_kernel"))]
+    ends = [i for i, r in enumerate(rows) if r[2].startswith(("adam_kernel", "adam_table_kernel",
+                                                                "adam_table_step_kernel"))]
     if len(ends) < back + 1:
         print("not enough steps")
         return

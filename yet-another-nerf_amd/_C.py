@@ -33,7 +33,8 @@ PREC_F32X3 = 2  # fp32 as three bf16 terms, six bf16 MFMAs per product (include/
 EXPORTS = (
     "yanerf_last_error", "yanerf_version", "yanerf_build_id", "yanerf_raygen", "yanerf_mlp_num_params",
     "yanerf_mlp_packed_bytes",
-    "yanerf_mlp_pack", "yanerf_mlp_saved_bytes", "yanerf_mlp_bwd_workspace_bytes", "yanerf_mlp_forward",
+    "yanerf_mlp_pack", "yanerf_mlp_pack_multi", "yanerf_mlp_saved_bytes", "yanerf_mlp_bwd_workspace_bytes",
+    "yanerf_mlp_forward",
     "yanerf_mlp_backward", "yanerf_mlp_backward_phase", "yanerf_composite_forward", "yanerf_composite_backward",
     "yanerf_composite_train", "yanerf_sample_pdf",
     "yanerf_refine", "yanerf_rgb_loss", "yanerf_adam", "yanerf_adam_scalars", "yanerf_adam_table", "yanerf_step_advance",
@@ -87,6 +88,7 @@ def lib():
         "yanerf_mlp_num_params": (c_int, [POINTER(MlpDesc)]),
         "yanerf_mlp_packed_bytes": (i64, [POINTER(MlpDesc), c_int]),
         "yanerf_mlp_pack": (c_int, [POINTER(MlpDesc), c_int, P, P, P]),
+        "yanerf_mlp_pack_multi": (c_int, [c_int, POINTER(MlpDesc), c_int, P, P, P]),
         "yanerf_mlp_saved_bytes": (i64, [POINTER(MlpDesc), c_int, i64]),
         "yanerf_mlp_bwd_workspace_bytes": (i64, [POINTER(MlpDesc), c_int, i64]),
         "yanerf_mlp_forward": (c_int, [POINTER(MlpDesc), c_int, P, P, P, P, i64, i64, P, P, P, P]),

@@ -340,25 +340,26 @@ static MlpLayout make_layout(const yanerf_mlp_desc* d, int prec) {
 // ============================================================================================ pack
 struct PackJob {
   const float* src;
-  int src_rows, src_ld;
-  int64_t dst_off;  // elements (T section) or floats (fp32 section)
-  int rows, cols;
-  int seg0, seg1_start, seg1_len;
-  int transpose, is_f32;
-  int64_t elem_base;
+  void* dst;            // the job's first output: the model's T section + dst_off elements, or its fp32 section + dst_off
+  int32_t elem_base;    // the job's first element in the launch's element space (4-column groups, jobs back to back)
+  int32_t t_plane;      // x3: elements per bf16 plane of the job's model
+  int16_t src_rows, src_ld, rows, cols;
+  int16_t seg0, seg1_start, seg1_len;
+  uint8_t transpose, is_f32;
 };
-constexpr int kMaxPackJobs = 3 * MAXL + 12;
+// one launch packs up to this many jobs (two default-size MLPs: 2 x 35); 40 B each keeps the kernel arguments < 4 KB
+constexpr int kMaxPackJobs = 96;
 struct PackJobs {
   PackJob j[kMaxPackJobs];
   int n;
-  int64_t total;
+  int32_t total;
 };
 
 // One thread per 4 consecutive columns of one row of a job (every job's cols is a multiple of 4, so a group never
 // straddles jobs or rows, and in fragment order its 4 outputs are contiguous: c % EPC runs over an aligned 4 of EPC).
+// The jobs of several MLPs (the trainer's coarse and fine models) go in one launch.
 template <typename T>
-__global__ void pack_kernel(PackJobs jobs, typename Cfg<T>::w_t* __restrict__ dst_t, float* __restrict__ dst_f,
-                            int64_t t_plane) {
+__global__ void pack_kernel(PackJobs jobs) {
   const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (e0 >= jobs.total) return;
   int lo = 0, hi = jobs.n - 1;
@@ -368,7 +369,8 @@ __global__ void pack_kernel(PackJobs jobs, typename Cfg<T>::w_t* __restrict__ ds
   }
   const PackJob& J = jobs.j[lo];
   const int64_t local0 = e0 - J.elem_base;
-  const int r = (int)(local0 / J.cols), c0 = (int)(local0 % J.cols);
+  const int cols = J.cols;
+  const int r = (int)(local0 / cols), c0 = (int)(local0 % cols);
   float v[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -381,13 +383,13 @@ __global__ void pack_kernel(PackJobs jobs, typename Cfg<T>::w_t* __restrict__ ds
     v[i] = (sk >= 0 && n < J.src_rows) ? J.src[(int64_t)n * J.src_ld + sk] : 0.0f;
   }
   if (J.is_f32) {
-    *(f4*)(dst_f + J.dst_off + local0) = f4{v[0], v[1], v[2], v[3]};
+    *(f4*)((float*)J.dst + local0) = f4{v[0], v[1], v[2], v[3]};
     return;
   }
   // GEMM operands are stored in MFMA A-fragment order: for each 16-row tile and 64-byte K-block, 64 lanes x 16 B,
   // lane = 16 * (k-chunk) + (row within the tile), so one wave-wide 16-byte load reads 1 KiB contiguously
   constexpr int KB = Cfg<T>::KB, EPC = Cfg<T>::EPC;
-  const int64_t fi = (((int64_t)(r >> 4) * (J.cols / KB) + c0 / KB) * 64 + ((c0 % KB) / EPC) * 16 + (r & 15)) * EPC +
+  const int64_t fi = (((int64_t)(r >> 4) * (cols / KB) + c0 / KB) * 64 + ((c0 % KB) / EPC) * 16 + (r & 15)) * EPC +
                      c0 % EPC;
   if constexpr (is_x3<T>) {
     // three bf16 planes, x = x0 + x1 + x2 exactly (each residual is exact in fp32)
@@ -402,14 +404,14 @@ __global__ void pack_kernel(PackJobs jobs, typename Cfg<T>::w_t* __restrict__ ds
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) {
       const uint2 w = {(uint32_t)x[pl][0] | ((uint32_t)x[pl][1] << 16), (uint32_t)x[pl][2] | ((uint32_t)x[pl][3] << 16)};
-      *(uint2*)(dst_t + pl * t_plane + J.dst_off + fi) = w;
+      *(uint2*)((bf16_t*)J.dst + (int64_t)pl * J.t_plane + fi) = w;
     }
   } else if constexpr (sizeof(T) == 4) {
-    *(f4*)(dst_t + J.dst_off + fi) = f4{v[0], v[1], v[2], v[3]};
+    *(f4*)((float*)J.dst + fi) = f4{v[0], v[1], v[2], v[3]};
   } else {
     const uint2 w = {(uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
                      (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)};
-    *(uint2*)(dst_t + J.dst_off + fi) = w;
+    *(uint2*)((bf16_t*)J.dst + fi) = w;
   }
 }
 
@@ -2756,16 +2758,29 @@ static int64_t param_numel(const MlpLayout& L, int i) {
   }
 }
 
-static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, const float* const* prm, PackJobs& J) {
-  J.n = 0;
-  J.total = 0;
+// appends one model's jobs to J (which may already hold another model's); nonzero when they do not fit one launch
+static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, int precision, const float* const* prm,
+                           void* packed, PackJobs& J) {
+  (void)d;
+  char* tsec = (char*)packed;
+  float* fsec = (float*)(tsec + L.f_base);
+  const int64_t tsize = precision == YANERF_PREC_F32 ? 4 : 2;
+  int fail = 0;
   auto add = [&](const float* src, int src_rows, int src_ld, int64_t dst_off, int rows, int cols, int seg0,
                  int seg1_start, int seg1_len, int transpose, int is_f32) {
+    if (J.n >= kMaxPackJobs || (int64_t)J.total + (int64_t)rows * cols > INT32_MAX) {
+      fail = 1;
+      return;
+    }
     PackJob& j = J.j[J.n++];
-    j.src = src; j.src_rows = src_rows; j.src_ld = src_ld; j.dst_off = dst_off; j.rows = rows; j.cols = cols;
-    j.seg0 = seg0; j.seg1_start = seg1_start; j.seg1_len = seg1_len; j.transpose = transpose; j.is_f32 = is_f32;
+    j.src = src;
+    j.dst = is_f32 ? (void*)(fsec + dst_off) : (void*)(tsec + dst_off * tsize);
     j.elem_base = J.total;
-    J.total += (int64_t)rows * cols;  // cols % 4 == 0 for every job (pack_kernel's 4-column groups)
+    j.t_plane = (int32_t)L.t_plane;
+    j.src_rows = (int16_t)src_rows; j.src_ld = (int16_t)src_ld; j.rows = (int16_t)rows; j.cols = (int16_t)cols;
+    j.seg0 = (int16_t)seg0; j.seg1_start = (int16_t)seg1_start; j.seg1_len = (int16_t)seg1_len;
+    j.transpose = (uint8_t)transpose; j.is_f32 = (uint8_t)is_f32;
+    J.total += rows * cols;  // cols % 4 == 0 for every job (pack_kernel's 4-column groups)
   };
   const int nl = L.L;
   for (int l = 0; l < nl; ++l) {
@@ -2794,7 +2809,7 @@ static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, const f
   add(h[6], L.cdim, L.hdir, L.wo_off, CMAX, HC, L.hdir, 0, 0, 0, 1);
   add(h[6], L.cdim, L.hdir, L.woh_off, 16, HC, L.hdir, 0, 0, 0, 0);
   add(h[7], 1, L.cdim, L.bo_off, 1, CMAX, L.cdim, 0, 0, 0, 1);
-  return 0;
+  return fail;
 }
 
 // point splits per dW tile. fp32 / x3 (at most 64): enough workgroups that the light jobs dispatched last fill the
@@ -3146,26 +3161,49 @@ int64_t yanerf_mlp_packed_bytes(const yanerf_mlp_desc* d, int precision) {
   return make_layout(d, precision).bytes;
 }
 
-int yanerf_mlp_pack(const yanerf_mlp_desc* d, int precision, const float* const* params, void* packed, void* stream) {
-  if (check_desc(d)) return 1;
-  YN_CHECK(precision == YANERF_PREC_F32 || precision == YANERF_PREC_BF16 || precision == YANERF_PREC_F32X3,
-           "mlp_pack: bad precision %d", precision);
-  YN_CHECK(params && packed, "mlp_pack: null pointer");
-  for (int i = 0; i < num_params(d); ++i) YN_CHECK(params[i], "mlp_pack: parameter %d is null", i);
-  MlpLayout L = make_layout(d, precision);
-  PackJobs J;
-  build_pack_jobs(d, L, params, J);
-  char* base = (char*)packed;
-  float* fsec = (float*)(base + L.f_base);
+static int launch_pack(const PackJobs& J, int precision, void* stream) {
+  if (J.total == 0) return 0;
   dim3 grid((unsigned)((J.total / 4 + 255) / 256)), block(256);
   if (precision == YANERF_PREC_F32)
-    hipLaunchKernelGGL(pack_kernel<float>, grid, block, 0, as_stream(stream), J, (float*)base, fsec, L.t_plane);
+    hipLaunchKernelGGL(pack_kernel<float>, grid, block, 0, as_stream(stream), J);
   else if (precision == YANERF_PREC_BF16)
-    hipLaunchKernelGGL(pack_kernel<bf16_t>, grid, block, 0, as_stream(stream), J, (bf16_t*)base, fsec, L.t_plane);
+    hipLaunchKernelGGL(pack_kernel<bf16_t>, grid, block, 0, as_stream(stream), J);
   else
-    hipLaunchKernelGGL(pack_kernel<x3_t>, grid, block, 0, as_stream(stream), J, (bf16_t*)base, fsec, L.t_plane);
+    hipLaunchKernelGGL(pack_kernel<x3_t>, grid, block, 0, as_stream(stream), J);
   YN_LAUNCH_CHECK("mlp_pack");
   return 0;
+}
+
+int yanerf_mlp_pack(const yanerf_mlp_desc* d, int precision, const float* const* params, void* packed, void* stream) {
+  return yanerf_mlp_pack_multi(1, d, precision, &params, &packed, stream);
+}
+
+int yanerf_mlp_pack_multi(int n_models, const yanerf_mlp_desc* d, int precision, const float* const* const* params,
+                          void* const* packed, void* stream) {
+  YN_CHECK(n_models >= 1 && d && params && packed, "mlp_pack_multi: bad arguments");
+  YN_CHECK(precision == YANERF_PREC_F32 || precision == YANERF_PREC_BF16 || precision == YANERF_PREC_F32X3,
+           "mlp_pack: bad precision %d", precision);
+  for (int m = 0; m < n_models; ++m) {
+    if (check_desc(d + m)) return 1;
+    YN_CHECK(params[m] && packed[m], "mlp_pack: null pointer (model %d)", m);
+    for (int i = 0; i < num_params(d + m); ++i) YN_CHECK(params[m][i], "mlp_pack: parameter %d is null", i);
+  }
+  PackJobs J;
+  J.n = 0;
+  J.total = 0;
+  for (int m = 0; m < n_models; ++m) {
+    const MlpLayout L = make_layout(d + m, precision);
+    const PackJobs before = J;
+    if (build_pack_jobs(d + m, L, precision, params[m], packed[m], J)) {
+      // this model's jobs do not fit beside the ones already collected: flush those, then retry it alone
+      YN_CHECK(before.n > 0, "mlp_pack: one model's jobs exceed a launch");
+      if (launch_pack(before, precision, stream)) return 1;
+      J.n = 0;
+      J.total = 0;
+      YN_CHECK(!build_pack_jobs(d + m, L, precision, params[m], packed[m], J), "mlp_pack: jobs exceed a launch");
+    }
+  }
+  return launch_pack(J, precision, stream);
 }
 
 int64_t yanerf_mlp_saved_bytes(const yanerf_mlp_desc* d, int precision, int64_t n_points) {

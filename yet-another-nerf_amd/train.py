@@ -164,6 +164,12 @@ class NeRFTrainer:
             raise ValueError(f"NeRFTrainer: grad_exchange {self.grad_exchange!r} (bucketed | single)")
         self.grad_ptrs = [_C.ptr_array([p.grad.data_ptr() for p in ps]) for ps in self.params]
         self.param_ptrs = [_C.ptr_array([p.data_ptr() for p in ps]) for ps in self.params]
+        # both models' packs in one launch (yanerf_mlp_pack_multi): the descriptors, the per-model parameter tables and
+        # the packed buffers as the C arrays it takes
+        self._pack_descs = (_C.MlpDesc * len(self.specs))(*[s.desc() for s in self.specs])
+        self._pack_params = _C.ptr_array([ctypes.addressof(t) for t in self.param_ptrs])
+        self._pack_dst = _C.ptr_array([t.data_ptr() for t in self.packed])
+        self._pack_prec = {s.precision for s in self.specs}
         self.events: Optional[Dict[str, List]] = None  # optional per-phase timing probes
         self.kernel_probes = False  # serialise the backward kernels (per-kernel timing; see step())
         self.fused_composite = True  # yanerf_composite_train per pass (False: the three separate launches)
@@ -187,6 +193,17 @@ class NeRFTrainer:
         self._eval_ws: Dict[int, Dict[str, torch.Tensor]] = {}
 
     TAB_STEPS = 1024  # Adam schedule rows uploaded at a time
+
+    def _pack(self, st):
+        """Pack both models' current parameters into their kernel layouts: one launch when they share a precision."""
+        L = _C.lib()
+        if len(self._pack_prec) == 1:
+            _C.check(L.yanerf_mlp_pack_multi(len(self.specs), self._pack_descs, self.specs[0].precision,
+                                             self._pack_params, self._pack_dst, st), "yanerf_mlp_pack_multi")
+            return
+        for i, s in enumerate(self.specs):
+            _C.check(L.yanerf_mlp_pack(ctypes.byref(s.desc()), s.precision, self.param_ptrs[i], _p(self.packed[i]),
+                                       st), "yanerf_mlp_pack")
 
     # --------------------------------------------------------------------------------------- device step state
     def _lr_of_step(self, it: int) -> float:
@@ -316,10 +333,9 @@ class NeRFTrainer:
             inj_ids = inj_ids.to(self.dev, torch.int64).reshape(1, R).contiguous()
         if inj_jit is not None:
             inj_jit = inj_jit.to(self.dev, F32).reshape(1, R, self.Pc).contiguous()
-        # pack the current parameters into the kernel layout (both models)
-        for i, s in enumerate(self.specs):
-            _C.check(L.yanerf_mlp_pack(ctypes.byref(s.desc()), s.precision, self.param_ptrs[i], _p(self.packed[i]),
-                                       st), "yanerf_mlp_pack")
+        # pack the current parameters into the kernel layout (both models, one launch; on the side stream beside the
+        # ray generation it measured slower: profiles/r5_ab_pack_launches.txt)
+        self._pack(st)
         # rays: uniform pixel sampling without replacement + stratified depths (Philox, or injected draws)
         seed, off = self.rng.next(R * self.Pc)
         jmode = 0 if not self.stratified else (1 if inj_jit is not None else 2)
@@ -631,9 +647,7 @@ class NeRFTrainer:
         far = self.far if far is None else float(far)
         pose = pose.reshape(1, -1, 4)[:, :3, :4].contiguous()
         focal = focal.reshape(1).contiguous()
-        for i, s in enumerate(self.specs):
-            _C.check(L.yanerf_mlp_pack(ctypes.byref(s.desc()), s.precision, self.param_ptrs[i], _p(self.packed[i]),
-                                       st), "yanerf_mlp_pack")
+        self._pack(st)
         world, rank = parallel.world_rank() if shard else (1, 0)
         rows = parallel.shard_range(H, rank, world)
         p0, n = rows.start * W, len(rows) * W

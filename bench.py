@@ -328,6 +328,26 @@ def extras(pcfg, cfg, dev, poses, focal, image, precision, others=()):
         "step_mfma_frac": round(train_flops_per_ray(Pc4, Pf4) * R4 / dt / 1e12 / PEAK_TFLOPS["bf16"], 4),
         "fine_fwd_ms": round(f4ms, 4), "fine_fwd_mfma_frac": round(fwd4 / (f4ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"], 4)}
     del tr
+    # SURVEY §8(d)'s large-batch roofline variant: the same Lego 64 + 128 step at 16,384 and 65,536 rays per step (the
+    # per-step fixed costs -- packs, ray generation, composites, refinement, reduces, Adam, launch gaps -- amortised
+    # over 4-16x the MLP work), bf16's default schedule; fp32 at 16,384 rays
+    out["lego_large_batch_train"] = {"config": "Lego 800x800, 64 + 128, one GPU, synthetic target"}
+    for p, R_big in (("bf16", 16384), ("bf16", 65536), ("fp32", 16384)):
+        tr = NeRFTrainer(pcfg, precision=p, device=dev, n_rays=R_big)
+        for i in range(2):
+            tr.step(poses[i:i + 1], focal, image)
+        torch.cuda.synchronize()
+        nst = 6
+        t0 = time.perf_counter()
+        for i in range(nst):
+            tr.step(poses[(2 + i) % len(poses)][None], focal, image)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / nst
+        out["lego_large_batch_train"][f"{p}_{R_big}"] = {
+            "rays_per_step": R_big, "rays_per_s": round(R_big / dt, 1), "ms_per_step": round(1e3 * dt, 3),
+            "step_mfma_frac": round(train_flops_per_ray(tr.Pc, tr.Pf) * R_big / dt / 1e12 / PEAK_TFLOPS[p], 4)}
+        del tr
+        torch.cuda.empty_cache()
     # the fused step captured as a HIP graph (NeRFTrainer.capture_step / replay_step: bit-equal to the eager step,
     # tests/test_gpu_trainer.py::test_graph_replayed_steps_equal_eager_steps), eager vs replayed ms per step
     out["graph_step"] = {}
@@ -459,7 +479,10 @@ def psnr_leg(precision: str, steps: int, dev):
     "Sometimes this is not enough") this scene's training collapses to the transparent solution for seed 42 -- no
     density anywhere, each ray's colour painted on its background-opacity last sample (`rays_before_far_plane` 0,
     profiles/r4_density_collapse_probe.jsonl). The headline PSNR is therefore the run with the density-layer bias
-    initialised to 1.0, which reconstructs the scene; the reference-init run and the bf16 run are reported beside it."""
+    initialised to 1.0, which reconstructs the scene; the reference-init run and the bf16 run are reported beside it.
+    Round 5: the reference itself, run in the build container on this scene at 50 x 50 (1,024 rays, 1,000 steps,
+    profiles/r5_reference_collapse.jsonl), collapses from its own init (20.45 dB, 0 rays before the far plane) and
+    reaches 33.95 dB from the bias-1.0 init; this build on the same runs: 20.48 / 33.90 dB (fp32), 33.81 dB (bf16)."""
     import tempfile
     sys.path.insert(0, str(ROOT / "tools"))
     from psnr_synthetic import run as psnr_run  # noqa: E402

@@ -619,6 +619,48 @@ def test_chunking_invariance(pkg, golden):
     assert torch.equal(a, b) and torch.equal(a, c)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3", "bf16"])
+def test_full_size_train_step_properties(pkg, precision):
+    """BASELINE configs[1]'s training step at its full size (Lego 800x800, 4096 rays, 64 + 128 samples, density noise)
+    through the drop-in registry path, where no oracle runs: size-independent properties of the whole step.
+    (1) Deterministic: the same seed gives bitwise-equal objectives and parameter gradients.
+    (2) The backward is exactly linear in the loss: the gradients of 2 x objective are bitwise 2 x those of the
+        objective (a power-of-two scale is exact through every fp32 product and sum, the fp32x3 planes, and the bf16
+        mode's per-tile power-of-two fp8 scales), so no stage of the backward adds, clamps or reorders by magnitude.
+    (3) Every gradient is finite, every parameter of both MLPs receives one, and the rasterised Monte-Carlo images
+        (when the config asks for them) are zero off the 4096 sampled pixels."""
+    from scene import synthetic_pose
+    pipe = _lego_pipeline(pkg, (3, 4), n_rays=4096, precision=precision)
+    pipe.train()
+    pose = torch.from_numpy(synthetic_pose(25.0, -30.0, 4.0)).float()[None, :3, :4].contiguous().to(DEV)
+    focal = torch.tensor([1111.111], device=DEV)
+    image = torch.rand(1, 800, 800, 3, device=DEV, generator=torch.Generator(device=DEV).manual_seed(9))
+    objs, grads = [], []
+    ops = pkg["ops"]
+    torch.manual_seed(17)
+    ops.RNG.next(0)  # the registry ops' Philox stream follows torch's seed; restart it at the same offset every run
+    state = ops.RNG.get_state()
+    for scale in (1.0, 1.0, 2.0):
+        torch.manual_seed(17)
+        ops.RNG.set_state(state)
+        pipe.zero_grad(set_to_none=True)
+        preds = pipe(poses=pose, focal_lengths=focal, image_rgb=image, evaluation_mode=pkg["EM"].TRAINING)
+        (preds["objective"].mean() * scale).backward()
+        objs.append(preds["objective"].detach().clone())
+        grads.append([p.grad.clone() if p.grad is not None else None for p in pipe.parameters()])
+        img = preds.get("rendered_images")
+    torch.cuda.synchronize()
+    assert torch.equal(objs[0], objs[1]) and torch.equal(objs[0], objs[2])
+    for i, (a, b, c) in enumerate(zip(*grads)):
+        assert a is not None, f"parameter {i} got no gradient"
+        assert torch.isfinite(a).all(), i
+        assert torch.equal(a, b), (precision, i, "not deterministic")
+        assert torch.equal(c, 2 * a), (precision, i, float((c - 2 * a).abs().max()))
+    if img is not None:  # output_rasterized_mc
+        lit = (img.detach().abs().sum(-1) > 0).sum().item()
+        assert lit <= 4096, lit
+
+
 # ------------------------------------------------------------------------------------------- checkpoints
 def test_trainer_checkpoint_interop(pkg, tmp_path):
     """The fused trainer writes the reference checkpoint format (run.py:409-414): a registry NeRFPipeline +

@@ -320,13 +320,15 @@ def test_refine_properties_large(pkg):
 
 
 # ------------------------------------------------------------------------------------------- full pipeline
-def _lego_pipeline(pkg, seeds, n_rays=4096, noise=0.2, precision="fp32"):
+def _lego_pipeline(pkg, seeds, n_rays=4096, noise=0.2, precision="fp32", n_fine=None):
     import yanerf_boot  # noqa: F401
     from yanerf_amd.utils.config import Config
     cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml")).pipeline
     cfg.ray_sampler.n_rays_per_image_sampled_from_mask = n_rays
     cfg.renderer.density_noise_std_train = noise
     cfg.model.precision = precision
+    if n_fine is not None:
+        cfg.renderer.n_pts_per_ray_fine_training = cfg.renderer.n_pts_per_ray_fine_evaluation = n_fine
     pipe = pkg["PIPELINES"].build(cfg).to(DEV)
     for f, s in zip(pipe.implicit_functions, seeds):
         f._fn.load_state_dict({k: torch.from_numpy(v) for k, v in make_nerf_mlp_params(LEGO_ARCH, int(s)).items()})
@@ -619,10 +621,11 @@ def test_chunking_invariance(pkg, golden):
     assert torch.equal(a, b) and torch.equal(a, c)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp32x3", "bf16"])
-def test_full_size_train_step_properties(pkg, precision):
-    """BASELINE configs[1]'s training step at its full size (Lego 800x800, 4096 rays, 64 + 128 samples, density noise)
-    through the drop-in registry path, where no oracle runs: size-independent properties of the whole step.
+@pytest.mark.parametrize("precision,n_fine", [("fp32", 128), ("fp32x3", 128), ("bf16", 128), ("bf16", 256)])
+def test_full_size_train_step_properties(pkg, precision, n_fine):
+    """BASELINE configs[1]'s training step at its full size (Lego 800x800, 4096 rays, 64 + 128 samples, density noise),
+    and configs[4]'s (bf16, 64 + 256), through the drop-in registry path, where no oracle runs: size-independent
+    properties of the whole step.
     (1) Deterministic: the same seed gives bitwise-equal objectives and parameter gradients.
     (2) The backward is exactly linear in the loss: the gradients of 2 x objective are bitwise 2 x those of the
         objective (a power-of-two scale is exact through every fp32 product and sum, the fp32x3 planes, and the bf16
@@ -630,7 +633,7 @@ def test_full_size_train_step_properties(pkg, precision):
     (3) Every gradient is finite, every parameter of both MLPs receives one, and the rasterised Monte-Carlo images
         (when the config asks for them) are zero off the 4096 sampled pixels."""
     from scene import synthetic_pose
-    pipe = _lego_pipeline(pkg, (3, 4), n_rays=4096, precision=precision)
+    pipe = _lego_pipeline(pkg, (3, 4), n_rays=4096, precision=precision, n_fine=n_fine)
     pipe.train()
     pose = torch.from_numpy(synthetic_pose(25.0, -30.0, 4.0)).float()[None, :3, :4].contiguous().to(DEV)
     focal = torch.tensor([1111.111], device=DEV)

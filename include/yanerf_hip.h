@@ -100,7 +100,9 @@ int64_t yanerf_mlp_packed_bytes(const yanerf_mlp_desc* d, int precision);
 int yanerf_mlp_pack(const yanerf_mlp_desc* d, int precision, const float* const* params, void* packed,
                     void* stream);
 /* yanerf_mlp_pack for several MLPs of one precision in ONE launch (the trainer's coarse and fine models every step):
- * d[m], params[m], packed[m] as yanerf_mlp_pack's for model m. Same bytes as n_models separate calls. */
+ * d[m], params[m], packed[m] as yanerf_mlp_pack's for model m. Same bytes as n_models separate calls. Not a reference
+ * entry point: the parameters are the two NeRFMLPs' (nerf_mlp.py:14-83) that the reference's renderer runs in turn
+ * (renderer.py:55-117). */
 int yanerf_mlp_pack_multi(int n_models, const yanerf_mlp_desc* d, int precision, const float* const* const* params,
                           void* const* packed, void* stream);
 /* Bytes of the per-call activation store kept from forward to backward for N points (0 for inference). */

@@ -410,13 +410,16 @@ def test_adam_matches_torch_adam(wd):
 @pytest.mark.parametrize("precision", ["fp32", "bf16", "fp32x3"])
 def test_pack_multi_equals_separate_packs(precision):
     """yanerf_mlp_pack_multi (both of the trainer's models in one launch) writes exactly the bytes of one
-    yanerf_mlp_pack per model -- two Lego-size MLPs, and a pair of different architectures (8 layers with a skip, and
-    4 layers without, 128 hidden) so the jobs of unlike layouts share the launch."""
+    yanerf_mlp_pack per model -- two Lego-size MLPs, a pair of different architectures (8 layers with a skip, and
+    4 layers without, 128 hidden) so the jobs of unlike layouts share the launch, and two 16-layer models whose jobs
+    exceed one launch (the first model's are flushed in a launch of their own)."""
     import ctypes
     from yanerf_amd import _C, ops
     from yanerf_amd.pipelines.models import MODELS
     L = _C.lib()
-    for archs in ((dict(), dict()), (dict(), dict(n_layers=4, input_skips=[], n_hidden_neurons_xyz=128))):
+    for archs in ((dict(), dict()), (dict(), dict(n_layers=4, input_skips=[], n_hidden_neurons_xyz=128)),
+                  # two 16-layer models: more jobs than one launch holds, so the pack flushes the first model's
+                  (dict(n_layers=16, input_skips=[5, 10]), dict(n_layers=16, input_skips=[8]))):
         models = []
         for i, kw in enumerate(archs):
             torch.manual_seed(10 + i)

@@ -126,3 +126,26 @@ def test_composite_noise_mode_needs_noise():
     assert L.yanerf_composite_train(ctypes.byref(o), d, d, d, d, None, None, d, d, 1, 4, 8, 3, 8, 8, 1.0, d, d, d, d,
                                     d, d, d, d, None) == 1
     assert "needs noise" in L.yanerf_last_error().decode()
+
+
+def test_mlp_pack_multi_validation():
+    """yanerf_mlp_pack_multi rejects an empty model list, a bad descriptor, a bad precision and null parameter /
+    buffer pointers before any launch (CPU: nothing reaches the device)."""
+    L = _C.lib()
+    d = (_C.MlpDesc * 2)(lego_desc(), lego_desc())
+    prm = (ctypes.c_void_p * 24)(*([16] * 24))
+    tables = _C.ptr_array([ctypes.addressof(prm), ctypes.addressof(prm)])
+    dst = _C.ptr_array([16, 16])
+    assert L.yanerf_mlp_pack_multi(0, d, _C.PREC_BF16, tables, dst, None) == 1
+    assert "bad arguments" in L.yanerf_last_error().decode()
+    assert L.yanerf_mlp_pack_multi(2, d, 7, tables, dst, None) == 1
+    assert "precision" in L.yanerf_last_error().decode()
+    bad = (_C.MlpDesc * 2)(lego_desc(), lego_desc(n_layers=0))
+    assert L.yanerf_mlp_pack_multi(2, bad, _C.PREC_BF16, tables, dst, None) == 1
+    assert "n_layers" in L.yanerf_last_error().decode()
+    assert L.yanerf_mlp_pack_multi(2, d, _C.PREC_BF16, tables, _C.ptr_array([16, 0]), None) == 1
+    assert "model 1" in L.yanerf_last_error().decode()
+    prm0 = (ctypes.c_void_p * 24)(*([16] * 23 + [0]))
+    assert L.yanerf_mlp_pack_multi(2, d, _C.PREC_BF16, _C.ptr_array([ctypes.addressof(prm), ctypes.addressof(prm0)]),
+                                   dst, None) == 1
+    assert "parameter 23 is null" in L.yanerf_last_error().decode()

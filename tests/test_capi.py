@@ -149,3 +149,20 @@ def test_mlp_pack_multi_validation():
     assert L.yanerf_mlp_pack_multi(2, d, _C.PREC_BF16, _C.ptr_array([ctypes.addressof(prm), ctypes.addressof(prm0)]),
                                    dst, None) == 1
     assert "parameter 23 is null" in L.yanerf_last_error().decode()
+
+
+def test_integration_stub_struct_matches_the_c_layout():
+    """The ctypes stub INTEGRATION.md shows a maintainer (its RaymarchOpts mirror) has the field names, offsets and size
+    of the binding the package uses, whose layout test_struct_layout_matches_c pins to the C header."""
+    import re
+    from pathlib import Path
+    text = (Path(__file__).resolve().parents[1] / "INTEGRATION.md").read_text()
+    block = re.search(r"```python\n(.*?)```", text[text.index("### ctypes stub"):], re.S).group(1)
+    src = block[block.index("class RaymarchOpts"):block.index("def composite_forward")]
+    ns = {"ctypes": ctypes}
+    exec(src, ns)
+    doc, ours = ns["RaymarchOpts"], _C.RaymarchOpts
+    assert ctypes.sizeof(doc) == ctypes.sizeof(ours)
+    assert [f[0] for f in doc._fields_] == [f[0] for f in ours._fields_]
+    for (name, _), (_, _) in zip(doc._fields_, ours._fields_):
+        assert getattr(doc, name).offset == getattr(ours, name).offset, name

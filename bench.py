@@ -6,6 +6,11 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
 
+`python bench.py --gpus N` with N > 1 and no launcher (no WORLD_SIZE in the environment) starts the N ranks itself:
+before anything touches the GPU it runs the second form above as a CHILD process (never an exec) and exits with its
+status, so an N-GPU invocation never degrades to a world-1 line (reference launch: scripts/run.py:162-166,
+runners/utils.py:216-238). Under a launcher, a WORLD_SIZE that differs from --gpus is an error (exit 2).
+
 A step = one rank's training step on one synthetic 800x800 image (4096 rays, 64 + (64+128) points per ray):
 raygen -> coarse MLP -> composite -> refine -> fine MLP -> composite -> loss -> backward (both MLPs) ->
 RCCL gradient all-reduce (two buckets, the coarse one overlapped with the fine MLP backward) -> Adam. Inputs (target image, poses) are resident in HBM before timing; weights are
@@ -28,6 +33,39 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(argv) -> int:
+    """`--gpus N` (N > 1) without a launcher: run this script under torch.distributed.run with N local ranks as a
+    child process and return its exit status (non-zero when any rank fails to start or dies: torch.distributed.run
+    tears the group down then). Called before torch is imported, so this process never initialises the GPU."""
+    import subprocess
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    n = pre.parse_known_args(argv)[0].gpus
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve()), *argv]
+    print(f"[bench] --gpus {n} without a launcher: starting {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def _needs_launch(argv) -> bool:
+    if "WORLD_SIZE" in os.environ:
+        return False
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    return pre.parse_known_args(argv)[0].gpus > 1
+
+
+if __name__ == "__main__" and _needs_launch(sys.argv[1:]):
+    sys.exit(launch_ranks(sys.argv[1:]))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -571,12 +609,20 @@ def main():
     ap.add_argument("--dist-selftest", action="store_true",
                     help="CPU/gloo check of the N-rank plumbing and its JSON fields (no GPU work; not a benchmark)")
     args = ap.parse_args()
+    env_world = parallel.env_rank_world()[1]
+    if env_world != args.gpus:
+        # never report an N-GPU run as some other world size
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks", file=sys.stderr)
+        sys.exit(2)
     if args.dist_selftest:
         return dist_selftest(args.steps)
+    backend = os.environ.get("YANERF_DIST_BACKEND") or "nccl"
+    if env_world > 1 and backend == "nccl" and torch.cuda.device_count() < env_world:
+        # RCCL needs one card per rank (a one-card rehearsal runs YANERF_DIST_BACKEND=gloo)
+        print(f"bench.py: {env_world} RCCL ranks but {torch.cuda.device_count()} visible GPUs", file=sys.stderr)
+        sys.exit(2)
 
     rank, world, local = parallel.init_distributed()
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     local = parallel.device_index(local)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)

@@ -85,7 +85,7 @@ def reference_sensitive_rays(sens, z_tol=2e-5):
 
 def split_gate(rgb, rgb_ref, z, z_ref, depth=None, depth_ref=None, *, fine_at=None, coarse=None, strict=1e-5,
                strict_depth=1e-4, z_tol=2e-5, tag="", sensitivity=None, same_tol=None, same_tol_depth=None,
-               all_vs_oracle=False, hip_exact=False):
+               all_vs_oracle=False, hip_exact=False, max_outside_without_weights=0):
     """coarse = (O, lengths [R,Pc], our coarse weights [R,Pc], n_fine): the oracle refinement of our coarse weights
     (deterministic, as the evaluation pass runs it) must equal z on every ray.
     same_tol / same_tol_depth: the bound on the rays whose refined depths agree with the reference's to z_tol (default
@@ -97,7 +97,11 @@ def split_gate(rgb, rgb_ref, z, z_ref, depth=None, depth_ref=None, *, fine_at=No
     equally valid fp32 evaluations of its coarse stage (set membership, asserted: none outside).
     hip_exact (the fp32 mode, whose coarse weights the golden's hip-arithmetic trial reproduces bit for bit): the rays
     with other depths must lie in that one trial's set -- the reference's own refinement of this build's coarse weights
-    moves exactly them."""
+    moves exactly them.
+    max_outside_without_weights: how many of those rays may lie outside every trial EXCEPT the weight-perturbation one
+    (trial (f) perturbs by this build's own measured coarse-weight error, so it is a diagnostic, not a bound on that
+    error): 0 in every mode but fp32x3 at the trained weights, whose bf16 MFMA is no IEEE fp32 sequence (measured 2 of
+    625 rays, round 5; the bound is that measurement, so a regression fails)."""
     R = len(z)
     rgb = np.asarray(rgb, np.float64).reshape(R, -1)
     rgb_ref = np.asarray(rgb_ref, np.float64).reshape(R, -1)
@@ -167,6 +171,7 @@ def split_gate(rgb, rgb_ref, z, z_ref, depth=None, depth_ref=None, *, fine_at=No
     if sensitivity is not None:
         # set membership: the reference itself moves every one of these rays under some valid fp32 evaluation
         assert report["rays_with_other_depths_outside_reference_sensitive"] == 0, report
+        assert report["outside_without_weights_trial"] <= max_outside_without_weights, report
         if hip_exact:
             assert report["outside_hip_arithmetic_trial"] == 0, report
     if flip.size:

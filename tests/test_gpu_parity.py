@@ -548,6 +548,17 @@ def test_scatter_rays_reference_error_behaviour(pkg):
             xb = t(bad)
             torch.zeros(1, 8, 3).scatter_(1, (xb[..., 0] + 4 * xb[..., 1]).long()[..., None].expand(-1, -1, 3).cpu(),
                                           v.cpu())
+    # the sticky device flag was cleared by the report: in-image scatters after it do not raise, and several scatters
+    # checked once (the pipeline's _rasterize_mc_samples) raise when any of them was outside
+    ref0 = torch.zeros(1, 8, 3, device=DEV).scatter_(1, (xy[..., 0] + 4 * xy[..., 1]).long()[..., None].expand(-1, -1, 3),
+                                                      v)
+    assert torch.equal(scatter_rays_to_image(v, xy, 2, 4).reshape(1, 8, 3), ref0)
+    from yanerf_amd import ops as _ops
+    _ops.scatter_rays(v, t([[[0, 0], [1, 0], [2, 5], [3, 1]]]), 2, 4, check=False)
+    _ops.scatter_rays(v, xy, 2, 4, check=False)
+    with pytest.raises(RuntimeError, match="outside"):
+        _ops.check_scatter_bounds(v.device)
+    _ops.check_scatter_bounds(v.device)
 
 
 def test_zero_outputer_known_answer(pkg, golden):

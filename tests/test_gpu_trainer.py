@@ -500,7 +500,8 @@ def test_trainer_render_matches_reference_render(golden, case):
         split_gate(n(f), g["fine_features"], z_gpu, z_ref, n(d), g["fine_depths"], fine_at=fine_at,
                    tag=f"render_eval {precision}" + ("" if case == "lego" else f" {case}"),
                    coarse=(O, n(zc), n(rb_w), 128), sensitivity=golden(f"sensitivity_{case}"),
-                   hip_exact=precision == "fp32", **loose_same)
+                   hip_exact=precision == "fp32",
+                   max_outside_without_weights=2 if (case, precision) == ("trained", "fp32x3") else 0, **loose_same)
 
 
 def tr_coarse_weights(tr, g, H, W, hw=800):
@@ -672,6 +673,34 @@ def test_multi_step_graph_equals_eager_steps(precision):
     assert graph.rng.get_state() == eager.rng.get_state()
     for a, b in ((eager.flat.data, graph.flat.data), (eager.exp_avg, graph.exp_avg), (eager.exp_avg_sq, graph.exp_avg_sq)):
         assert torch.equal(a, b)
+
+
+def test_multi_step_graph_replay_with_one_bound_keeps_the_other_per_step():
+    """replay_step(near=...) alone on a 2-step graph: the far side keeps each captured step's own row (not their
+    mean), and a 1-D near tensor of K values is one value per step -- bit for bit the eager steps fed those bounds."""
+    from scene import synthetic_pose
+    from yanerf_amd.train import NeRFTrainer
+    cfg = lego_cfg()
+    trs = [NeRFTrainer(cfg.pipeline, precision="fp32", device=DEV, n_rays=256, seed=5) for _ in range(2)]
+    img = torch.rand(1, 800, 800, 3, device=DEV, generator=torch.Generator(device=DEV).manual_seed(8))
+    poses = torch.stack([torch.from_numpy(synthetic_pose(30.0 * k, -30.0, 4.0)).float() for k in range(5)]).to(DEV)
+    focal = torch.tensor([1111.111], device=DEV)
+    near = torch.tensor([[2.0], [2.1], [1.9]])
+    far = torch.tensor([[6.0], [5.7], [6.2]])
+    near2 = torch.tensor([2.3, 1.8])  # 1-D, one value per captured step
+    eager, graph = trs
+    for t in trs:
+        t.step(poses[0:1], focal, img, near=near[0:1], far=far[0:1])
+    graph.capture_step(poses[1:3], focal, img, near=near[1:3], far=far[1:3], n_steps=2)
+    graph.replay_step(poses[1:3], focal)
+    for k in (1, 2):
+        eager.step(poses[k:k + 1], focal, img, near=near[k:k + 1], far=far[k:k + 1])
+    b = graph.replay_step(poses[3:5], focal, near=near2)
+    for j, k in enumerate((3, 4)):
+        a = eager.step(poses[k:k + 1], focal, img, near=float(near2[j]), far=far[1 + j:2 + j])
+    torch.cuda.synchronize()
+    assert torch.equal(a["sq_fine"], b["sq_fine"]) and torch.equal(a["sq_coarse"], b["sq_coarse"])
+    assert torch.equal(eager.flat.data, graph.flat.data)
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])

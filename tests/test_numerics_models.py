@@ -109,6 +109,11 @@ def test_split_gate_asserts_set_membership(tmp_path, monkeypatch):
     with pytest.raises(AssertionError):
         split_gate(rgb, rgb, z, z_ref, sensitivity=sens, tag="cpu-outside", **kw)
     sens["max_z_move_weights"] = np.array([0, 1, 0, 0], np.float32)
+    # inside the weight-perturbation trial alone: a diagnostic, not a bound -- allowed only when budgeted
+    with pytest.raises(AssertionError):
+        split_gate(rgb, rgb, z, z_ref, sensitivity=sens, tag="cpu-weights-only", **kw)
+    split_gate(rgb, rgb, z, z_ref, sensitivity=sens, tag="cpu-weights-only", max_outside_without_weights=1, **kw)
+    sens["max_z_move"] = np.array([0, 1, 0, 0], np.float32)
     split_gate(rgb, rgb, z, z_ref, sensitivity=sens, tag="cpu-inside", **kw)
     with pytest.raises(AssertionError):
         split_gate(rgb, rgb, z, z_ref, sensitivity=sens, tag="cpu-hip-exact", hip_exact=True, **kw)

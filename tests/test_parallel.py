@@ -144,3 +144,41 @@ def test_bench_distributed_fields_gloo_world2():
     assert len(info["allreduce_exposed_ms_per_rank"]) == 2 and info["allreduce_exposed_ms_max"] >= 0
     assert info["grad_exchange"] == "bucketed" and info["grad_bytes"] == 4 * 1_191_688
     assert info["selftest_grad_ok"]
+
+
+def _run_bench_plain(extra, timeout=300):
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(root / "bench.py")] + extra, capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd="/tmp")
+    return r
+
+
+def test_bench_gpus_n_starts_its_own_ranks():
+    """`python bench.py --gpus 2` with NO launcher starts two ranks itself (a child torch.distributed.run, before any
+    GPU call) and rank 0's line reports the two-rank group: an N-GPU invocation never degrades to a world-1 line
+    (reference launch: scripts/run.py:162-166)."""
+    import json
+    r = _run_bench_plain(["--gpus", "2", "--steps", "2", "--dist-selftest"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["distributed"]["world_size"] == 2 and d["distributed"]["selftest_grad_ok"]
+
+
+def test_bench_world_size_mismatch_fails():
+    """A launcher that started another number of ranks than --gpus asks for is an error, not a warning."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--dist-selftest"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

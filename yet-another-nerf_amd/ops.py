@@ -412,14 +412,39 @@ def rgb_loss(pred: torch.Tensor, image: torch.Tensor, xys: torch.Tensor, scale: 
     return sq, g
 
 
+_OOB_FLAGS: dict = {}  # device -> sticky int32 out-of-image flag of yanerf_scatter_rays (set by the kernel, never cleared
+# by it; cleared here when it is reported)
+
+
+def _oob_flag(dev) -> torch.Tensor:
+    f = _OOB_FLAGS.get(dev)
+    if f is None:
+        f = _OOB_FLAGS[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return f
+
+
+def check_scatter_bounds(dev) -> None:
+    """Raise if any yanerf_scatter_rays call on `dev` since the last check met a pixel index outside its image (one
+    host read-back for any number of scatter calls; skipped while a stream is being captured into a graph)."""
+    f = _OOB_FLAGS.get(dev)
+    if f is None or torch.cuda.is_current_stream_capturing():
+        return
+    if int(f.item()):
+        f.zero_()
+        raise RuntimeError("scatter_rays_to_image: a ray's pixel index x + W * y lies outside the image (torch's "
+                           "scatter_ raises on it: index out of bounds)")
+
+
 @torch.no_grad()
 def scatter_rays(values: torch.Tensor, xys: torch.Tensor, image_height: int, image_width: int,
-                 bg_color: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 bg_color: Optional[torch.Tensor] = None, check: bool = True) -> torch.Tensor:
     """scatter_rays_to_image (pipelines/utils.py:299-323) on the device: values [B, *spatial, C] at integer-valued
     xys [B, *spatial, 2] onto a new [B, H, W, C] image filled with bg_color (when its last dim is C) or zeros. A host
     bg_color (the reference's own test passes a CPU tensor) is moved to the device; one whose last dim is not C is
-    ignored, as the reference ignores it. A pixel index outside the image raises, as the reference's scatter_ does
-    (the kernel flags it on the device; this reads the flag back)."""
+    ignored, as the reference ignores it. A pixel index outside the image raises, as the reference's scatter_ does:
+    the kernel sets a sticky per-device flag and `check_scatter_bounds` reads it back -- here when `check` (a caller
+    scattering several tensors at the same xys passes check=False for all but the last: one host sync, not one per
+    tensor)."""
     if bg_color is not None and bg_color.shape[-1] != values.shape[-1]:
         bg_color = None
     if bg_color is not None and not bg_color.is_cuda:
@@ -437,12 +462,10 @@ def scatter_rays(values: torch.Tensor, xys: torch.Tensor, image_height: int, ima
                                       "passes None); only a [C] background is supported")
         bg = _f32c(bg_color.reshape(C))
     out = torch.empty(B, int(image_height), int(image_width), C, dtype=_F32, device=v.device)
-    oob = torch.zeros(1, dtype=torch.int32, device=v.device)
     _C.check(_C.lib().yanerf_scatter_rays(_p(v), _p(xy), B, v.shape[1], C, int(image_height), int(image_width),
-                                          _p(bg), _p(out), _p(oob), _stream()), "yanerf_scatter_rays")
-    if int(oob.item()):
-        raise RuntimeError(f"scatter_rays_to_image: a ray's pixel index x + W * y lies outside the {int(image_height)} "
-                           f"x {int(image_width)} image (torch's scatter_ raises on it: index out of bounds)")
+                                          _p(bg), _p(out), _p(_oob_flag(v.device)), _stream()), "yanerf_scatter_rays")
+    if check:
+        check_scatter_bounds(v.device)
     return out if values.dtype == _F32 else out.to(values.dtype)
 
 

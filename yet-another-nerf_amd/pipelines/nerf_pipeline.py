@@ -20,7 +20,7 @@ from .ray_samplers import RAY_SAMPLERS
 from .ray_samplers.utils import RenderSamplingMode
 from .renderers import RENDERERS
 from .renderers.utils import RendererOutput
-from .utils import EvaluationMode, PartialFunctionWrapper, RayBundle, ViewMetrics, sample_grid, scatter_rays_to_image
+from .utils import EvaluationMode, PartialFunctionWrapper, RayBundle, ViewMetrics, sample_grid
 
 logger = logging.getLogger(__name__)
 
@@ -145,7 +145,13 @@ class NeRFPipeline(torch.nn.Module):
     def _rasterize_mc_samples(self, xys, bg_color, image_height, image_width, rendered):
         if image_height is None or image_width is None:
             image_height, image_width = self.render_image_height, self.render_image_width
-        return {k: scatter_rays_to_image(v, xys, image_height, image_width, bg_color) for k, v in rendered.items()}
+        # scatter_rays_to_image per tensor (nerf_pipeline.py:307-324), with ONE read-back of the kernels' out-of-image
+        # flag for all of them (the same xys) instead of one host sync per tensor
+        from .. import ops
+        out = {k: ops.scatter_rays(v, xys, image_height, image_width, bg_color, check=False) for k, v in rendered.items()}
+        if out:
+            ops.check_scatter_bounds(xys.device)
+        return out
 
 
 def _chunk_generator(chunk_size: int, origins, directions, lengths, xys, bg_color=None, *args, **kwargs):

@@ -538,28 +538,34 @@ class NeRFTrainer:
             return x.expand(K, *x.shape[1:])
         raise ValueError(f"NeRFTrainer: {name} has {x.shape[0]} rows for {K} captured steps")
 
-    @staticmethod
-    def _host_bounds_key(near, far):
+    def _host_bounds_key(self, near, far):
         """The (near, far) rows of host-side bounds (floats or CPU tensors: LLFF's per-image bounds come from the
         loader on the host), so a replay with the same values skips rewriting the graph's static bounds buffer (its
-        fill launches cost ~10 us each on a ~1 ms step); None when either is a device tensor or missing."""
+        fill launches cost ~10 us each on a ~1 ms step); None when either is a device tensor or missing. The rows are
+        read as _set_graph_bounds reads them."""
+        K = self._g_K
         out = []
         for v in (near, far):
             if v is None or (isinstance(v, torch.Tensor) and v.device.type != "cpu"):
                 return None
-            out.append(tuple(v.float().reshape(v.shape[0] if v.dim() > 1 else 1, -1).mean(-1).tolist())
-                       if isinstance(v, torch.Tensor) else float(v))
+            if isinstance(v, torch.Tensor):
+                per_step = v.dim() > 1 or (K > 1 and v.dim() == 1 and v.numel() == K)
+                out.append(tuple(v.float().reshape(v.shape[0] if per_step else 1, -1).mean(-1).tolist()))
+            else:
+                out.append(float(v))
         return tuple(out)
 
     def _set_graph_bounds(self, near, far):
         """Write the depth range of the captured steps into the static [K, 2] buffer: None = the config's value;
-        floats; tensors averaged per step (ray_sampler.py:280-283; [K, ...] rows, or one value for every step) -- host
-        tensors on the host, device tensors on the device (no host sync)."""
+        floats; tensors averaged per step (ray_sampler.py:280-283) -- [K, ...] rows (one per captured step), a 1-D
+        tensor of K values when K > 1 (one per step), or any other shape = one image's bounds, averaged into one value
+        for every step -- host tensors on the host, device tensors on the device (no host sync)."""
         K = self._g_bounds.shape[0]
         for i, (v, dflt) in enumerate(((near, self.near), (far, self.far))):
             v = dflt if v is None else v
             if isinstance(v, torch.Tensor):
-                v = v.float().reshape(v.shape[0] if v.dim() > 1 else 1, -1).mean(-1)
+                per_step = v.dim() > 1 or (K > 1 and v.dim() == 1 and v.numel() == K)
+                v = v.float().reshape(v.shape[0] if per_step else 1, -1).mean(-1)
                 if v.numel() not in (1, K):
                     raise ValueError(f"NeRFTrainer: {v.numel()} depth bounds for {K} captured steps")
                 if v.device.type == "cpu":
@@ -582,7 +588,8 @@ class NeRFTrainer:
         if near is not None or far is not None:
             key = self._host_bounds_key(near, far)
             if key is None or key != self._g_bounds_key:  # host bounds equal to the previous replay's: nothing to write
-                cur = (self._g_bounds[:, 0].clone(), self._g_bounds[:, 1].clone())
+                # the side not given keeps its per-step rows ([K, 1]: one row per captured step, not one image's bounds)
+                cur = (self._g_bounds[:, 0:1].clone(), self._g_bounds[:, 1:2].clone())
                 self._set_graph_bounds(cur[0] if near is None else near, cur[1] if far is None else far)
                 self._g_bounds_key = key
         if pose is not None:

@@ -109,6 +109,13 @@ int yanerf_mlp_pack_multi(int n_models, const yanerf_mlp_desc* d, int precision,
 int64_t yanerf_mlp_saved_bytes(const yanerf_mlp_desc* d, int precision, int64_t n_points);
 /* Bytes of the backward workspace for N points (gradient rows + split-K partial slabs). */
 int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, int64_t n_points);
+/* The split-K plan of the weight gradients for N points (host-only query, no device work): dW tiles per launch, point
+ * splits per tile, points per stage, and the fewest / most stages one split reduces (split s covers stages
+ * [n s / S, n (s + 1) / S)). Not a reference entry point: the reduction over points the reference's autograd does
+ * inside each Linear backward (nerf_mlp.py:267-289) -- reported by the full-size parity tests so the regime they
+ * exercise is visible. */
+int yanerf_mlp_dw_plan(const yanerf_mlp_desc* d, int precision, int64_t n_points, int* tiles, int* splits,
+                       int64_t* stage_points, int64_t* stages_min, int64_t* stages_max);
 
 /* Forward over R rays x P samples (point p = r*P + j at x = o_r + t_rj * d_r, models/utils.py:244).
  *   origins/directions [R][3], lengths [R][P] -> sigma_raw [R][P] (density before ReLU), rgb [R][P][C].

@@ -520,10 +520,13 @@ def render_two_pass(params_c, params_f, arch, cfg: RenderCfg, origins, direction
 
 
 def train_step_grads(params_c, params_f, arch, cfg: RenderCfg, origins, directions, lengths, gt_rgb,
-                     noise_c, noise_f, pdf_u, z_fine=None, relu_masks=None, abs_terms: bool = False):
+                     noise_c, noise_f, pdf_u, z_fine=None, relu_masks=None, abs_terms: bool = False,
+                     loss_rays: Optional[int] = None):
     """One training step's objective and parameter gradients (nerf_pipeline.py:181-213, 284-305; apis.py:87-88):
     objective = mse(fine) + mse(coarse); noise_* already include density_noise_std. abs_terms=True adds each gradient
-    element's sum of absolute term values (abs_fine / abs_coarse, nerf_mlp_backward)."""
+    element's sum of absolute term values (abs_fine / abs_coarse, nerf_mlp_backward). loss_rays: the number of rays the
+    mean-squared error averages over when these rays are one chunk of a larger step (the gradients of a step are sums
+    over its rays, so chunks' gradients add up; the objective is this chunk's own)."""
     R = lengths.shape[0]
     out = render_two_pass(params_c, params_f, arch, cfg, origins, directions, lengths, noise_c=noise_c,
                           noise_f=noise_f, pdf_u=pdf_u, random_sampling=True, z_fine=z_fine,
@@ -531,7 +534,7 @@ def train_step_grads(params_c, params_f, arch, cfg: RenderCfg, origins, directio
     gt = gt_rgb.reshape(R, 3)
     mse_f = rgb_metrics(gt[None], out["fine"][0][None])["rgb_mse"]
     mse_c = rgb_metrics(gt[None], out["coarse"][0][None])["rgb_mse"]
-    scale = f32(2.0 / (R * 3))
+    scale = f32(2.0 / ((R if loss_rays is None else int(loss_rays)) * 3))
     grads, absg = [], []
     for stage, params, cache, ctx in (("fine", params_f, out["cache_f"], out["ctx_f"]),
                                       ("coarse", params_c, out["cache_c"], out["ctx_c"])):

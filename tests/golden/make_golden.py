@@ -181,6 +181,29 @@ def gen_mlp(out):
         out[f"mlp_{tag}"] = d
 
 
+def gen_mlp_bf16ref(out):
+    """The reference's Lego NeRFMLP on mlp_lego's inputs under torch.autocast("cpu", bfloat16) -- its own
+    reduced-precision behaviour (bf16 Linear layers, fp32 elsewhere) -- with the same upstream gradients: outputs and
+    parameter gradients on mlp_lego's entries. The bf16 mode's gates are bounded by this error against the fp32
+    reference (tests/test_gpu_parity.py)."""
+    g = np.load(HERE / "mlp_lego.npz")
+    model, _ = build_mlp(LEGO_ARCH, int(g["seed"]))
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        res = model(torch.from_numpy(g["origins"]), torch.from_numpy(g["directions"]), torch.from_numpy(g["lengths"]))
+    sig, rgb = res["rays_densities"].float(), res["rays_features"].float()
+    model.zero_grad()
+    ((sig * torch.from_numpy(g["g_sigma"])).sum() + (rgb * torch.from_numpy(g["g_rgb"])).sum()).backward()
+    d = dict(sigma=np32(sig), rgb=np32(rgb))
+    for name, p in model.named_parameters():
+        gr = np32(p.grad).reshape(-1)
+        if f"grad:{name}" in g.files:
+            d[f"grad:{name}"] = gr.reshape(p.shape)
+        else:
+            d[f"gradval:{name}"] = gr[g[f"gradidx:{name}"]]
+            d[f"gradsum:{name}"] = np.array([gr.astype(np.float64).sum(), np.linalg.norm(gr.astype(np.float64))])
+    out["mlp_lego_bf16ref"] = d
+
+
 def gen_raymarcher(out):
     g = torch.Generator().manual_seed(3)
     R, P = 37, 64
@@ -407,10 +430,10 @@ def fern_pipeline_cfg(n_fine, n_rays=1024):
     return p
 
 
-def record_eval_render(pipe, pose, focal, H, W, **bounds):
+def record_eval_render(pipe, pose, focal, H, W, subset=None, **bounds):
     """The reference's two-pass EVALUATION render through its renderer, with the per-stage outputs: coarse features /
     depths / weights, the refined depths (RayPointRefiner, recorded through a pass-through wrapper) and the fine
-    features / depths."""
+    features / depths. subset: render only these rays (flat indices into the H x W grid) of the sampler's bundle."""
     refined = []
     orig_fwd = RayPointRefiner.forward
 
@@ -423,12 +446,15 @@ def record_eval_render(pipe, pose, focal, H, W, **bounds):
     try:
         rb = pipe.ray_sampler(pose, focal, evaluation_mode=EvaluationMode.EVALUATION, image_height=H, image_width=W,
                               **bounds)
+        if subset is not None:
+            sel = torch.as_tensor(np.asarray(subset, np.int64))
+            rb = type(rb)(*[x.reshape(x.shape[0], -1, *x.shape[3:])[:, sel] for x in rb])
         with torch.no_grad():
             ro = pipe.renderer(*rb, bg_color=None, implicit_functions=pipe.implicit_functions,
                                evaluation_mode=EvaluationMode.EVALUATION)
     finally:
         RayPointRefiner.forward = orig_fwd
-    R = H * W
+    R = H * W if subset is None else len(subset)
     pv = ro.prev_stage
     return dict(lengths=np32(rb.lengths).reshape(R, -1), coarse_features=np32(pv.features).reshape(R, -1),
                 coarse_depths=np32(pv.depths).reshape(R), coarse_weights=np32(pv.aux["weights"]).reshape(R, -1),
@@ -610,6 +636,8 @@ def perturbed_refiner_weights(delta, rng):
         RayPointRefiner.forward = orig
 
 
+STRIDED_800 = (np.arange(2048) * (800 * 800 // 2048) + 157).astype(np.int64)  # test_full_image_800_vs_oracle's rays
+
 # measured max |coarse weight (this build) - coarse weight (reference)| on the gated renders, fp32 and fp32x3 builds,
 # Lego 16 x 16, Fern 9 x 12, trained 25 x 25 (tools/dump_coarse_stage.py; profiles/r5_coarse_weight_deltas.json)
 WEIGHT_DELTA = 1.8e-7
@@ -637,6 +665,10 @@ def gen_sensitivity(out):
                       dict(min_depth=torch.tensor([[FERN_NEAR]]), max_depth=torch.tensor([[FERN_FAR]]))))
     cases.append(("trained", lego_pipeline_cfg(H=TRAINED_HW, W=TRAINED_HW), "trained", torch.from_numpy(TRAINED_POSE)[None],
                   torch.tensor([TRAINED_FOCAL], dtype=torch.float32), TRAINED_GRID, TRAINED_GRID, {}))
+    # BASELINE configs[1]'s evaluation image at full size: the 2,048 strided rays of the 800 x 800 Lego camera that
+    # tests/test_gpu_trainer.py::test_full_image_800_vs_oracle gates (base render stored with the trials)
+    cases.append(("lego_800", lego_pipeline_cfg(), (11, 12), torch.from_numpy(synthetic_pose(30.0, -30.0, 4.0))[None],
+                  torch.tensor([1111.1111]), 800, 800, dict(subset=STRIDED_800)))
     if os.environ.get("YANERF_SENSITIVITY_ONLY"):
         cases = [c for c in cases if c[0] == os.environ["YANERF_SENSITIVITY_ONLY"]]
 
@@ -650,7 +682,7 @@ def gen_sensitivity(out):
         load_pipeline_weights(pipe, seeds)
         pipe.eval()
         base = record_eval_render(pipe, pose, focal, H, W, **bounds)
-        R = H * W
+        R = H * W if "subset" not in bounds else len(bounds["subset"])
         dz, drgb = np.zeros(R), np.zeros(R)
 
         def note(r):
@@ -689,8 +721,9 @@ def gen_sensitivity(out):
         dz_e, dz_f = np.zeros(R), np.zeros(R)
         lib = _hip_order_lib()
         # the whole fp32 coarse stage as the HIP kernels evaluate it: correctly rounded embedding, the MFMA chain of
-        # every Linear, the composite's arithmetic (its coarse weights equal this build's bit for bit:
-        # tests/test_gpu_parity.py::test_hip_arithmetic_trial_reproduces_coarse_weights); then the reference's own
+        # every Linear, the composite's arithmetic (its coarse weights equal this build's bit for bit: asserted in
+        # test_gpu_parity.py::test_render_eval_lego, test_gpu_fern.py::test_fern_render_with_tensor_bounds_vs_reference and
+        # test_gpu_trainer.py::test_trainer_render_matches_reference_render / test_full_image_800_vs_oracle); then the reference's own
         # RayPointRefiner / sample_pdf on them
         with hip_order_model(coarse, lib, pe="cr"), hip_raymarcher():
             r = record_eval_render(pipe, pose, focal, H, W, **bounds)
@@ -709,7 +742,7 @@ def gen_sensitivity(out):
         pipe.double()
         try:
             r64 = record_eval_render(pipe, pose.double(), focal.double(), H, W,
-                                     **{k: v.double() for k, v in bounds.items()})
+                                     **{k: (v.double() if torch.is_tensor(v) else v) for k, v in bounds.items()})
         finally:
             torch.set_default_dtype(torch.float32)
             pipe.float()
@@ -718,7 +751,9 @@ def gen_sensitivity(out):
             z_fine=base["z_fine"], fine_features=base["fine_features"], z_fine_f64=r64["z_fine"].astype(np.float64),
             fine_features_f64=r64["fine_features"].astype(np.float64), max_z_move_hip_order=dz_e.astype(np.float32),
             max_z_move_weights=dz_f.astype(np.float32), weight_delta=np.float32(WEIGHT_DELTA),
-            hip_arithmetic_coarse_weights=hip_w)
+            hip_arithmetic_coarse_weights=hip_w,
+            **({} if "subset" not in bounds else dict(subset=np.asarray(bounds["subset"], np.int64), pose=np32(pose),
+                                                      focal=np32(focal), **{f"base_{k}": v for k, v in base.items()})))
 
 
 # Parity at TRAINED weights: the Lego architecture trained 1,500 fused fp32 steps (tools/density_collapse_probe.py: seed
@@ -790,6 +825,76 @@ def replay_draws(log):
 TRAJ_HW, TRAJ_RAYS, TRAJ_STEPS = 32, 256, 20
 
 
+def _trajectory_setup():
+    """gen_train_trajectory's fixed inputs: the runner config, pipeline config, focal, per-step poses / images, seeds."""
+    cfg = Config.fromfile(str(REF / "configs/nerf/lego.yml"))
+    pcfg = lego_pipeline_cfg(n_rays=TRAJ_RAYS, H=TRAJ_HW, W=TRAJ_HW)
+    focal = torch.tensor([0.5 * TRAJ_HW / np.tan(0.5 * 0.6911112070083618)], dtype=torch.float32)
+    views = [(-180.0 + 360.0 * k / TRAJ_STEPS, -30.0 + 10.0 * np.sin(k)) for k in range(TRAJ_STEPS)]
+    poses = [torch.from_numpy(synthetic_pose(th, ph, 4.0))[None] for th, ph in views]
+    images = [torch.from_numpy(np.ascontiguousarray(scene_view(th, ph, TRAJ_HW)))[None].float() for th, ph in views]
+    return cfg.runner, pcfg, focal, poses, images, (61, 62)
+
+
+def _trajectory_run(setup, dtype, draws=None, autocast=False):
+    """The reference's registry pipeline trained TRAJ_STEPS steps by the reference runner's Adam and schedule (see
+    gen_train_trajectory). draws: per-step Recorder logs to replay (None: draw and record). autocast: every step's
+    forward under torch.autocast("cpu", bfloat16). Returns (pipeline, logs, losses [steps, 3], lrs)."""
+    from yanerf.runners.utils import create_lr_scheduler, warmup_lr_scheduler
+    runner, pcfg, focal, poses, images, seeds = setup
+    torch.set_default_dtype(dtype)
+    try:
+        pipe = PIPELINES.build(pcfg)
+        load_pipeline_weights(pipe, seeds)
+        pipe.to(dtype)
+        pipe.train()
+        opt = torch.optim.Adam([{"params": pipe.parameters(), "init_lr": runner.init_lr}], lr=runner.init_lr,
+                               weight_decay=runner.weight_decay)
+        sched = create_lr_scheduler(opt, runner)
+        torch.manual_seed(70)
+        rec, logs, losses, lrs = Recorder(), [], [], []
+        for it in range(TRAJ_STEPS):
+            sched(iter=it)
+            if runner["warmup_steps"] > 0 and it <= runner["warmup_steps"]:
+                warmup_lr_scheduler(opt, it, runner["warmup_steps"], runner["warmup_lr"])
+            lrs.append(opt.param_groups[0]["lr"])
+            opt.zero_grad()
+            kw = dict(poses=poses[it].to(dtype), focal_lengths=focal.to(dtype), image_rgb=images[it].to(dtype),
+                      evaluation_mode=EvaluationMode.TRAINING)
+            if draws is None:
+                rec.log = []
+                with rec.capture():
+                    preds = pipe(**kw)
+                logs.append(list(rec.log))
+            elif autocast:
+                with replay_draws(draws[it]), torch.autocast("cpu", dtype=torch.bfloat16):
+                    preds = pipe(**kw)
+            else:
+                with replay_draws(draws[it]):
+                    preds = pipe(**kw)
+            preds["objective"].mean().backward()
+            opt.step()
+            losses.append([float(preds["objective"].mean()), float(preds["loss_rgb_mse"].mean()),
+                           float(preds["loss_prev_stage_rgb_mse"].mean())])
+        return pipe, logs, np.array(losses, np.float64), np.array(lrs, np.float64)
+    finally:
+        torch.set_default_dtype(torch.float32)
+
+
+def _trajectory_params(d, prefix, pipe):
+    """Parameters after the trajectory: whole tensors up to 4,096 elements, a fixed 256-entry sample of the others."""
+    for i, f in enumerate(pipe.implicit_functions):
+        for name, p in f._fn.named_parameters():
+            v = p.detach().double().numpy()
+            if v.size <= 4096:
+                d[f"{prefix}{i}:{name}"] = v.astype(np.float32 if prefix == "param" else np.float64)
+            else:
+                idx = np.random.Generator(np.random.PCG64(len(name) * 1000 + i)).choice(v.size, 256, replace=False)
+                if prefix == "param":
+                    d[f"paramidx{i}:{name}"] = idx.astype(np.int64)
+                d[f"{prefix}{i}:{name}"] = v.reshape(-1)[idx].astype(np.float32 if prefix == "param" else np.float64)
+
+
 def gen_train_trajectory(out):
     """Multi-step training parity: the reference's registry pipeline (lego.yml: 64 + 128 samples, density noise 0.2) with
     the reference runner's optimizer and schedule (scripts/run.py:158-160: torch.optim.Adam over create_param_groups,
@@ -801,54 +906,10 @@ def gen_train_trajectory(out):
     parameters after the last step (whole tensors up to 4,096 elements, a fixed 256-entry sample of the larger ones).
     The same trajectory is then re-run by the reference in float64 on the recorded draws: the exact algorithm's
     parameters after the same steps, the yardstick both fp32 implementations are measured against."""
-    from yanerf.runners.utils import create_lr_scheduler, warmup_lr_scheduler
-    cfg = Config.fromfile(str(REF / "configs/nerf/lego.yml"))
-    runner = cfg.runner
-    pcfg = lego_pipeline_cfg(n_rays=TRAJ_RAYS, H=TRAJ_HW, W=TRAJ_HW)
-    focal = torch.tensor([0.5 * TRAJ_HW / np.tan(0.5 * 0.6911112070083618)], dtype=torch.float32)
-    views = [(-180.0 + 360.0 * k / TRAJ_STEPS, -30.0 + 10.0 * np.sin(k)) for k in range(TRAJ_STEPS)]
-    poses = [torch.from_numpy(synthetic_pose(th, ph, 4.0))[None] for th, ph in views]
-    images = [torch.from_numpy(np.ascontiguousarray(scene_view(th, ph, TRAJ_HW)))[None].float() for th, ph in views]
-    seeds = (61, 62)
-
-    def run(dtype, draws=None):
-        torch.set_default_dtype(dtype)
-        try:
-            pipe = PIPELINES.build(pcfg)
-            load_pipeline_weights(pipe, seeds)
-            pipe.to(dtype)
-            pipe.train()
-            opt = torch.optim.Adam([{"params": pipe.parameters(), "init_lr": runner.init_lr}], lr=runner.init_lr,
-                                   weight_decay=runner.weight_decay)
-            sched = create_lr_scheduler(opt, runner)
-            torch.manual_seed(70)
-            rec, logs, losses, lrs = Recorder(), [], [], []
-            for it in range(TRAJ_STEPS):
-                sched(iter=it)
-                if runner["warmup_steps"] > 0 and it <= runner["warmup_steps"]:
-                    warmup_lr_scheduler(opt, it, runner["warmup_steps"], runner["warmup_lr"])
-                lrs.append(opt.param_groups[0]["lr"])
-                opt.zero_grad()
-                kw = dict(poses=poses[it].to(dtype), focal_lengths=focal.to(dtype), image_rgb=images[it].to(dtype),
-                          evaluation_mode=EvaluationMode.TRAINING)
-                if draws is None:
-                    rec.log = []
-                    with rec.capture():
-                        preds = pipe(**kw)
-                    logs.append(list(rec.log))
-                else:
-                    with replay_draws(draws[it]):
-                        preds = pipe(**kw)
-                preds["objective"].mean().backward()
-                opt.step()
-                losses.append([float(preds["objective"].mean()), float(preds["loss_rgb_mse"].mean()),
-                               float(preds["loss_prev_stage_rgb_mse"].mean())])
-            return pipe, logs, np.array(losses, np.float64), np.array(lrs, np.float64)
-        finally:
-            torch.set_default_dtype(torch.float32)
-
-    pipe, logs, losses, lrs = run(torch.float32)
-    pipe64, _, losses64, _ = run(torch.float64, logs)
+    setup = _trajectory_setup()
+    _, _, focal, poses, images, seeds = setup
+    pipe, logs, losses, lrs = _trajectory_run(setup, torch.float32)
+    pipe64, _, losses64, _ = _trajectory_run(setup, torch.float64, logs)
     d = dict(seeds=np.array(seeds), n_rays=np.int64(TRAJ_RAYS), hw=np.int64(TRAJ_HW), steps=np.int64(TRAJ_STEPS),
              focal=np32(focal), poses=np.concatenate([np32(p) for p in poses]),
              images=np.concatenate([np32(i) for i in images]), losses=losses, losses_f64=losses64, lrs=lrs)
@@ -860,18 +921,30 @@ def gen_train_trajectory(out):
         d[f"noise_coarse:{it}"] = np32(log[2][1])
         d[f"pdf_u:{it}"] = np32(log[3][1])
         d[f"noise_fine:{it}"] = np32(log[4][1])
-    for i, (f, f64) in enumerate(zip(pipe.implicit_functions, pipe64.implicit_functions)):
-        p64 = dict(f64._fn.named_parameters())
-        for name, p in f._fn.named_parameters():
-            v, v64 = p.detach().numpy().astype(np.float32), p64[name].detach().numpy().astype(np.float64)
-            if v.size <= 4096:
-                d[f"param{i}:{name}"], d[f"param64_{i}:{name}"] = v, v64
-            else:
-                idx = np.random.Generator(np.random.PCG64(len(name) * 1000 + i)).choice(v.size, 256, replace=False)
-                d[f"paramidx{i}:{name}"] = idx.astype(np.int64)
-                d[f"param{i}:{name}"] = v.reshape(-1)[idx]
-                d[f"param64_{i}:{name}"] = v64.reshape(-1)[idx]
+    _trajectory_params(d, "param", pipe)
+    _trajectory_params(d, "param64_", pipe64)
     out["train_trajectory"] = d
+
+
+def gen_train_trajectory_bf16ref(out):
+    """The reference's own bf16 trajectory: gen_train_trajectory's 20 steps on the SAME recorded draws (read from the
+    committed train_trajectory.npz), every forward under torch.autocast("cpu", bfloat16), the reference's own
+    refinement of its bf16 coarse weights. Per-step losses and the parameters after the last step on the trajectory
+    golden's entries: the bound of the bf16 mode's trajectory test (tests/test_gpu_trainer.py)."""
+    g = np.load(HERE / "train_trajectory.npz")
+    logs = []
+    for it in range(TRAJ_STEPS):
+        logs.append([("multinomial", torch.from_numpy(g[f"pixel_ids:{it}"])),
+                     ("rand_like", torch.from_numpy(g[f"jitter_u:{it}"])),
+                     ("randn_like", torch.from_numpy(g[f"noise_coarse:{it}"])),
+                     ("rand", torch.from_numpy(g[f"pdf_u:{it}"])),
+                     ("randn_like", torch.from_numpy(g[f"noise_fine:{it}"]))])
+    pipe, _, losses, lrs = _trajectory_run(_trajectory_setup(), torch.float32, logs, autocast=True)
+    assert np.array_equal(lrs, g["lrs"])
+    d = dict(losses=losses)
+    _trajectory_params(d, "param", pipe)
+    d = {k: v for k, v in d.items() if not k.startswith("paramidx")}  # the trajectory golden's entries
+    out["train_trajectory_bf16ref"] = d
 
 
 def gen_zero_outputer(out):
@@ -1105,10 +1178,225 @@ def gen_iter_runner(out):
     out["iter_runner"] = d
 
 
+# ----------------------------------------------------------------------------- BASELINE configs[1] at full size
+FULL_RAYS = 4096  # lego.yml:77 n_rays_per_image_sampled_from_mask
+FULL_TIE_REL = 2e-6  # ReLU tie candidates recorded: |pre-activation| <= FULL_TIE_REL * max |pre-activation| of the layer
+FULL_SAMPLE = 256  # entries sampled per large gradient tensor (as record_train_step)
+
+
+def relu_hash_coeffs(P: int, U: int) -> np.ndarray:
+    """[P * U, 2] float64 integer coefficients of the per-ray ReLU-decision hash (relu_ray_hash): two independent
+    sets, each in [1, 2^31). Test side: tests/test_gpu_fullsize.py builds the same arrays."""
+    rng = np.random.Generator(np.random.PCG64(7000 + 1000 * P + U))
+    return rng.integers(1, 2 ** 31, size=(P * U, 2), dtype=np.int64).astype(np.float64)
+
+
+def relu_ray_hash(mask: np.ndarray, R: int, P: int) -> np.ndarray:
+    """[R, 2] per-ray hashes of one layer's ReLU decisions mask [R * P, U]: sum over the ray's (point, unit) pairs with
+    decision 1 of the pair's two coefficients. Every partial sum is an integer below 2^53, so the float64 matmul is
+    exact in any summation order (the GPU test recomputes it with torch and compares for equality). One flipped
+    decision changes both sums."""
+    U = mask.shape[-1]
+    return mask.reshape(R, P * U).astype(np.float64) @ relu_hash_coeffs(P, U)
+
+
+def gen_train_step_lego_4096(out):
+    """BASELINE configs[1]'s training step at its full size, through the reference: lego.yml's pipeline (4096 rays,
+    64 + 128 samples, density noise 0.2, 800 x 800) on one synthetic camera, every random draw recorded (pixel ids,
+    jitter, both noise draws, refinement uniforms), the coarse weights and refined depths, per-ray coarse / fine outputs,
+    the objective and losses, and the parameter gradients (whole tensors up to 4,096 elements, a fixed 256-entry sample
+    plus the sum / norm of the larger ones, as record_train_step). The ReLU decisions (786,432 fine points x 2,304 units)
+    are too large to commit, so they are recorded as (a) two exact integer hashes per ray and layer (relu_ray_hash) and
+    (b) every unit whose pre-activation lies within FULL_TIE_REL of its layer's largest, with the reference's decision
+    there: a GPU test that finds the hashes of a ray different can rebuild the reference's decisions of that ray from
+    its own plus these candidates, and must reproduce the hash (so the two differ only at fp32 ties).
+    Then, on the same draws and the reference's refined depths:
+      * the reference re-run in float64 (the exact algorithm's gradients: the EXACT_RATIO yardstick);
+      * the reference under torch.autocast("cpu", bfloat16) (its own reduced-precision gradients: the bf16 gates'
+        reference-derived bound);
+      * the oracle under the reference's own ReLU decisions (O_ref of parity_gates.tie_budget_gate, in 512-ray chunks
+        whose gradients add up) with each element's sum of |terms|, pinned here to the reference's gradients."""
+    sys.path.insert(0, str(HERE.parents[1]))
+    from oracle import nerf_oracle as O
+    R = FULL_RAYS
+    pcfg = lego_pipeline_cfg()
+    assert int(pcfg.ray_sampler.n_rays_per_image_sampled_from_mask) == R
+    seeds = (81, 82)
+    pose = torch.from_numpy(synthetic_pose(15.0, -35.0, 4.0))[None]
+    focal = torch.tensor([1111.1111])
+    img = torch.rand(1, 800, 800, 3, generator=torch.Generator().manual_seed(18))
+    Pc, Pf = 64, 192
+
+    def build(dtype=torch.float32):
+        pipe = PIPELINES.build(pcfg)
+        load_pipeline_weights(pipe, seeds)
+        pipe.to(dtype)
+        pipe.train()
+        return pipe
+
+    # ---- the fp32 step, every draw and the ReLU pre-activations recorded
+    pipe = build()
+    rec = Recorder()
+    refined = []
+    orig_ref = RayPointRefiner.forward
+
+    def rec_fwd(self, origins, directions, lengths, xys, ray_weights):
+        rb = orig_ref(self, origins, directions, lengths, xys, ray_weights)
+        refined.append((ray_weights.detach().clone(), rb.lengths.detach().clone()))
+        return rb
+
+    masks, cands, hashes, stage_out = {}, {}, {}, []
+    hooks = [pipe.renderer.register_forward_hook(lambda m, i, o: stage_out.append(o))]
+    for k, f in enumerate(pipe.implicit_functions):
+        mods = [(li, layer[1]) for li, layer in enumerate(f._fn.xyz_encoder.mlp)] + [(8, f._fn.color_layer[1])]
+        for li, mod in mods:
+            def hook(m, inp, k=k, li=li):  # a PRE-hook: the reference's ReLUs are in place
+                pre = inp[0].detach().reshape(-1, inp[0].shape[-1]).numpy().copy()
+                P = Pc if k == 0 else Pf
+                mk = pre > 0
+                masks[(k, li)] = mk
+                hashes[(k, li)] = relu_ray_hash(mk, R, P)
+                a = np.abs(pre)
+                idx = np.flatnonzero(a <= FULL_TIE_REL * a.max())
+                cands[(k, li)] = (idx.astype(np.int64), mk.reshape(-1)[idx], (a.reshape(-1)[idx] / a.max()).astype(
+                    np.float32))
+            hooks.append(mod.register_forward_pre_hook(hook))
+    RayPointRefiner.forward = rec_fwd
+    torch.manual_seed(19)
+    try:
+        with rec.capture():
+            preds = pipe(poses=pose, focal_lengths=focal, image_rgb=img, evaluation_mode=EvaluationMode.TRAINING)
+    finally:
+        RayPointRefiner.forward = orig_ref
+        for h in hooks:
+            h.remove()
+    preds["objective"].mean().backward()
+    kinds = [n for n, _ in rec.log]
+    assert kinds == ["multinomial", "rand_like", "randn_like", "rand", "randn_like"], kinds
+    ids = rec.log[0][1].numpy().astype(np.int64)
+    z_fine = np32(refined[0][1]).reshape(R, Pf)
+    fine_o, coarse_o = stage_out[-1], stage_out[-1].prev_stage
+    d = dict(pose=np32(pose), focal=np32(focal), seeds=np.array(seeds), n_rays=np.int64(R), H=np.int64(800),
+             W=np.int64(800), pixel_ids=ids, gt_rgb=np32(img.reshape(1, -1, 3)[0, ids[0]]),
+             jitter_u=np32(rec.log[1][1]), noise_coarse=np32(rec.log[2][1]), pdf_u=np32(rec.log[3][1]),
+             noise_fine=np32(rec.log[4][1]), coarse_weights=np32(refined[0][0]).reshape(R, Pc), z_fine=z_fine,
+             coarse_features=np32(coarse_o.features).reshape(R, 3), coarse_depths=np32(coarse_o.depths).reshape(R),
+             fine_features=np32(fine_o.features).reshape(R, 3), fine_depths=np32(fine_o.depths).reshape(R),
+             tie_rel=np.float32(FULL_TIE_REL))
+    for kk in ("objective", "loss_rgb_mse", "loss_prev_stage_rgb_mse"):
+        d[kk] = np32(preds[kk])
+    for (k, li), hsh in hashes.items():
+        d[f"relu_hash{k}:{li}"] = hsh
+        idx, dec, rel = cands[(k, li)]
+        d[f"relu_cand_idx{k}:{li}"], d[f"relu_cand_dec{k}:{li}"], d[f"relu_cand_rel{k}:{li}"] = idx, dec, rel
+
+    def sample_of(i, name, n):
+        return np.random.Generator(np.random.PCG64(len(name) * 1000 + i)).choice(n, size=FULL_SAMPLE, replace=False)
+
+    def put_grads(prefix, model_list):
+        for i, f in enumerate(model_list):
+            for name, p in f._fn.named_parameters():
+                gr = p.grad.detach().double().numpy().reshape(-1)
+                if gr.size <= 4096:
+                    d[f"{prefix}{i}:{name}"] = gr.astype(np.float64 if prefix == "grad64_" else np.float32)
+                else:
+                    sel = sample_of(i, name, gr.size)
+                    d[f"{prefix}idx{i}:{name}"] = sel.astype(np.int64)
+                    d[f"{prefix}val{i}:{name}"] = gr[sel].astype(np.float64 if prefix == "grad64_" else np.float32)
+                    d[f"{prefix}sum{i}:{name}"] = np.array([gr.sum(), np.linalg.norm(gr)])
+
+    put_grads("grad", pipe.implicit_functions)  # grad / gradidx / gradval / gradsum: the golden_grad_items layout
+    log = list(rec.log)
+    del pipe, preds, stage_out, fine_o, coarse_o
+    print("train_step_lego_4096: fp32 step recorded", flush=True)
+
+    def rerun(dtype, autocast=False):
+        """The same step on the recorded draws, the refined depths replaced by the fp32 reference's."""
+        torch.set_default_dtype(dtype)
+        try:
+            p2 = build(dtype)
+            zf = torch.from_numpy(z_fine).to(dtype)
+
+            def fixed(self, origins, directions, lengths, xys, ray_weights):
+                rb = orig_ref(self, origins, directions, lengths, xys, ray_weights)  # consumes the pdf_u draw
+                return rb._replace(lengths=zf.reshape(rb.lengths.shape))
+
+            RayPointRefiner.forward = fixed
+            try:
+                with replay_draws(log):
+                    if autocast:
+                        with torch.autocast("cpu", dtype=torch.bfloat16):
+                            pr = p2(poses=pose.to(dtype), focal_lengths=focal.to(dtype), image_rgb=img.to(dtype),
+                                    evaluation_mode=EvaluationMode.TRAINING)
+                    else:
+                        pr = p2(poses=pose.to(dtype), focal_lengths=focal.to(dtype), image_rgb=img.to(dtype),
+                                evaluation_mode=EvaluationMode.TRAINING)
+            finally:
+                RayPointRefiner.forward = orig_ref
+            pr["objective"].mean().backward()
+            return p2, float(pr["objective"].mean())
+        finally:
+            torch.set_default_dtype(torch.float32)
+
+    p64, obj64 = rerun(torch.float64)
+    put_grads("grad64_", p64.implicit_functions)
+    d["objective_f64"] = np.float64(obj64)
+    del p64
+    print("train_step_lego_4096: float64 re-run", flush=True)
+    pbf, objbf = rerun(torch.float32, autocast=True)
+    put_grads("grad_bf16ac", pbf.implicit_functions)
+    d["objective_bf16ac"] = np.float64(objbf)
+    del pbf
+    print("train_step_lego_4096: bf16 autocast re-run", flush=True)
+
+    # ---- the oracle under the reference's own ReLU decisions at its depths (O_ref), in 512-ray chunks
+    arch = O.MLPArch.from_dict(LEGO_ARCH)
+    pc, pf = make_nerf_mlp_params(LEGO_ARCH, seeds[0]), make_nerf_mlp_params(LEGO_ARCH, seeds[1])
+    cfg = O.RenderCfg(n_pts_fine=128, density_noise_std=0.2, raymarch=O.RaymarchOpts(background_density_bias=1e-6))
+    o, dd, z, _ = O.sample_rays_train(d["pose"], d["focal"], 800, 800, 2.0, 6.0, Pc, ids, d["jitter_u"])
+    o, dd, z = o.reshape(R, 3), dd.reshape(R, 3), z.reshape(R, Pc)
+    nc = (d["noise_coarse"].reshape(R, Pc) * np.float32(0.2)).astype(np.float32)
+    nf = (d["noise_fine"].reshape(R, Pf) * np.float32(0.2)).astype(np.float32)
+    acc = {}
+    C = 512
+    for r0 in range(0, R, C):
+        sl = slice(r0, r0 + C)
+
+        def mk(k, P):
+            rows = slice(r0 * P, (r0 + C) * P)
+            return dict(trunk=[masks[(k, li)][rows] for li in range(8)], color=masks[(k, 8)][rows])
+
+        res = O.train_step_grads(pc, pf, arch, cfg, o[sl], dd[sl], z[sl], d["gt_rgb"][sl], nc[sl], nf[sl],
+                                 d["pdf_u"].reshape(R, -1)[sl], z_fine=z_fine[sl], relu_masks=(mk(0, Pc), mk(1, Pf)),
+                                 abs_terms=True, loss_rays=R)
+        for key in ("grads_coarse", "grads_fine", "abs_coarse", "abs_fine"):
+            for name, v in res[key].items():
+                a = np.asarray(v, np.float64)
+                acc[(key, name)] = a if (key, name) not in acc else acc[(key, name)] + a
+        print(f"train_step_lego_4096: oracle rays {r0}..{r0 + C}", flush=True)
+    pin = 0.0
+    for i, key in ((0, "coarse"), (1, "fine")):
+        for name in pc:
+            g_or, ab = acc[(f"grads_{key}", name)].reshape(-1), acc[(f"abs_{key}", name)].reshape(-1)
+            if f"grad{i}:{name}" in d:
+                ref, sel = d[f"grad{i}:{name}"].astype(np.float64), slice(None)
+            else:
+                ref, sel = d[f"gradval{i}:{name}"].astype(np.float64), d[f"gradidx{i}:{name}"]
+            d[f"oref{i}:{name}"], d[f"oabs{i}:{name}"] = g_or[sel].astype(np.float64), ab[sel].astype(np.float64)
+            err = np.abs(g_or[sel] - ref)
+            M = max(np.abs(ref).max(), 1e-30)
+            assert (err <= 2e-5 * M + 2e-5 * ab[sel]).all(), (i, name, float(err.max() / M))
+            pin = max(pin, float(err.max() / M))
+    d["oracle_pin_max"] = np.float64(pin)
+    print(f"train_step_lego_4096: oracle pinned to the reference at {pin:.3e} x max", flush=True)
+    out["train_step_lego_4096"] = d
+
+
 GENERATORS = (gen_harmonic, gen_raysampler, gen_mlp, gen_raymarcher, gen_sample_pdf, gen_render_eval,
               gen_train_step, gen_zero_outputer, gen_init_checksums, gen_pipeline_state, gen_lr_schedule,
               gen_raysampler_masked, gen_iter_runner, gen_render_fern, gen_train_step_fern, gen_sensitivity,
-              gen_render_trained, gen_train_step_trained, gen_train_trajectory)
+              gen_render_trained, gen_train_step_trained, gen_train_trajectory, gen_train_step_lego_4096,
+              gen_mlp_bf16ref, gen_train_trajectory_bf16ref)
 
 
 def main():

@@ -72,6 +72,34 @@ def test_mlp_size_queries():
     assert L.yanerf_mlp_bwd_workspace_bytes(ctypes.byref(d), _C.PREC_BF16, 1 << 20) > 0
 
 
+def test_dw_plan_query():
+    """yanerf_mlp_dw_plan (host only): the split-K plan the backward launches with. At the headline fine pass (4096 rays
+    x 192 points) every split reduces hundreds of stages; every point is in exactly one split."""
+    d = lego_desc()
+    n = 4096 * 192
+    for prec in (_C.PREC_F32, _C.PREC_F32X3, _C.PREC_BF16):
+        p = _C.dw_plan(d, prec, n)
+        lo, hi = p["stages_per_split"]
+        assert p["tiles"] > 0 and 1 <= p["splits"] and lo <= hi <= lo + 1 and lo >= 100, (prec, p)
+        nst = -(-n // p["stage_points"])
+        assert lo * p["splits"] <= nst <= hi * p["splits"], (prec, p)
+    # bf16: whole rounds of one workgroup per CU, as many rounds as the fp8 scale slots need (configs[4]'s 320-point
+    # fine pass needs two)
+    b1, b2 = _C.dw_plan(d, _C.PREC_BF16, n), _C.dw_plan(d, _C.PREC_BF16, 4096 * 320)
+    assert b1["tiles"] * b1["splits"] <= 256 < b1["tiles"] * b2["splits"] <= 512, (b1, b2)
+    assert _C.dw_plan(d, _C.PREC_BF16, 48 * 192)["stages_per_split"][1] < 16  # the 48-ray golden: a few stages
+    assert L_error_on_bad_plan()
+
+
+def L_error_on_bad_plan() -> bool:
+    L = _C.lib()
+    i, s = ctypes.c_int(), ctypes.c_int()
+    a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    rc = L.yanerf_mlp_dw_plan(ctypes.byref(lego_desc()), 1, -5, ctypes.byref(i), ctypes.byref(s), ctypes.byref(a),
+                              ctypes.byref(b), ctypes.byref(c))
+    return rc == 1 and "n_points" in L.yanerf_last_error().decode()
+
+
 @pytest.mark.parametrize("bad,msg", [
     (dict(n_freq_xyz=11), "xyz embedding"), (dict(n_freq_dir=5), "dir embedding"), (dict(hidden_xyz=300), "xyz"),
     (dict(hidden_dir=256), "dir"), (dict(n_layers=0), "n_layers"), (dict(color_dim=5), "color_dim"),

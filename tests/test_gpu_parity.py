@@ -4,8 +4,9 @@ CPU oracle. Needs an MI355X: marked `gpu`.
 Tolerances (fp32 precision mode): per-stage RGB <= 1e-5 / depth <= 1e-4 (north star: 1e-4), composite / sample_pdf
 at float round-off; end-to-end fine stage through parity_gates.split_gate: strict on every ray whose refined depths
 agree with the ones the reference's coarse weights give, and every larger difference accounted for by a counted ray
-whose refined samples differ (the reference's sample_pdf `denom < eps` branch). bf16 mode is checked against loose
-bounds only (it is the throughput mode).
+whose refined samples differ (the reference's sample_pdf `denom < eps` branch). bf16 mode (the throughput mode) is
+bounded by the reference's OWN bf16 error: its NeRFMLP under torch.autocast("cpu", bfloat16) (mlp_lego_bf16ref.npz),
+at most BF16_VS_AUTOCAST x as far from the fp32 reference.
 """
 import numpy as np
 import pytest
@@ -122,13 +123,39 @@ def test_mlp_fwd_bwd_fp32(pkg, golden, tag, precision):
             close(np.linalg.norm(v.astype(np.float64)), nn, 1e-5 * max(1.0, nn), 1e-5)
 
 
+# bf16 mode gates, derived from the REFERENCE's own bf16 (mlp_lego_bf16ref.npz: its NeRFMLP under
+# torch.autocast("cpu", bfloat16) on mlp_lego's inputs): this build's bf16 mode (bf16 MFMA forward / dX, fp8 e4m3
+# saves and gradient rows, fp8 dW) may be at most BF16_VS_AUTOCAST x as far from the fp32 reference as the reference's
+# autocast is, per output and per gradient tensor (or within BF16_FLOOR relative L2 where autocast is nearly exact)
+BF16_VS_AUTOCAST = 2.0
+BF16_FLOOR = 2e-2
+
+
+def _rel_l2(v, ref):
+    v, ref = np.asarray(v, np.float64).reshape(-1), np.asarray(ref, np.float64).reshape(-1)
+    return float(np.linalg.norm(v - ref) / max(np.linalg.norm(ref), 1e-12))
+
+
+def bf16_grad_bound(golden) -> float:
+    """BF16_VS_AUTOCAST x the reference's worst per-tensor autocast gradient error on mlp_lego (relative L2): the bound
+    of the bf16 gradient tests that compare against the oracle at other shapes (measured 0.129 -> 0.258)."""
+    g, b = golden("mlp_lego"), golden("mlp_lego_bf16ref")
+    worst = max(_rel_l2(b[k], g[k]) for k in b if k.startswith(("grad:", "gradval:")))
+    return BF16_VS_AUTOCAST * worst
+
+
 def test_mlp_bf16_bounds(pkg, golden):
-    g = golden("mlp_lego")
+    """bf16 mode outputs on mlp_lego: RGB and sigma max error against the fp32 reference within BF16_VS_AUTOCAST x the
+    reference's own autocast error (measured autocast: RGB 3.1e-3, sigma 5.3e-3), gradient norms within 10 %."""
+    g, b = golden("mlp_lego"), golden("mlp_lego_bf16ref")
     m, _ = build_mlp(pkg, LEGO_ARCH, int(g["seed"]), precision="bf16")
     out = m(t(g["origins"]), t(g["directions"]), t(g["lengths"]))
-    # bf16 activations/weights, fp32 accumulate: loose bound vs the fp32 reference
-    close(n(out["rays_features"]), g["rgb"], 2e-2)
-    close(n(out["rays_densities"]), g["sigma"], 5e-2, 5e-2)
+    e = {k: float(np.abs(n(out[key]).reshape(-1) - g[k].reshape(-1)).max())
+         for k, key in (("rgb", "rays_features"), ("sigma", "rays_densities"))}
+    ac = {k: float(np.abs(b[k].reshape(-1) - g[k].reshape(-1)).max()) for k in ("rgb", "sigma")}
+    print(f"bf16 outputs: ours {e}, reference autocast {ac}")
+    for k in e:
+        assert e[k] <= BF16_VS_AUTOCAST * ac[k], (k, e[k], ac[k])
     m.zero_grad()
     ((out["rays_densities"] * t(g["g_sigma"])).sum() + (out["rays_features"] * t(g["g_rgb"])).sum()).backward()
     for name, p in m.named_parameters():
@@ -139,25 +166,26 @@ def test_mlp_bf16_bounds(pkg, golden):
 
 def test_mlp_bf16_gradients_elementwise(pkg, golden):
     """bf16 mode, every parameter gradient element against the fp32 reference: relative L2 error per tensor (on the
-    golden's full gradients, or its sampled elements for the large matrices). Catches layout errors in the saved /
-    gradient rows that the norm bound above would miss (a permuted row keeps the norm)."""
-    g = golden("mlp_lego")
+    golden's full gradients, or its sampled elements for the large matrices) within BF16_VS_AUTOCAST x the reference's
+    own autocast error on the same tensor (mlp_lego_bf16ref), or BF16_FLOOR. Catches layout errors in the saved /
+    gradient rows that the norm bound above would miss (a permuted row keeps the norm and gives > 1)."""
+    g, b = golden("mlp_lego"), golden("mlp_lego_bf16ref")
     m, _ = build_mlp(pkg, LEGO_ARCH, int(g["seed"]), precision="bf16")
     out = m(t(g["origins"]), t(g["directions"]), t(g["lengths"]))
     m.zero_grad()
     ((out["rays_densities"] * t(g["g_sigma"])).sum() + (out["rays_features"] * t(g["g_rgb"])).sum()).backward()
-    worst = 0.0
+    rep = {}
     for name, p in m.named_parameters():
         v = n(p.grad).astype(np.float64)
-        if f"grad:{name}" in g:
-            ref = g[f"grad:{name}"].astype(np.float64)
-        else:
-            ref = g[f"gradval:{name}"].astype(np.float64)
+        key = f"grad:{name}" if f"grad:{name}" in g else f"gradval:{name}"
+        if key.startswith("gradval"):
             v = v.reshape(-1)[g[f"gradidx:{name}"]]
-        rel = np.linalg.norm(v - ref) / max(np.linalg.norm(ref), 1e-12)
-        worst = max(worst, rel)
-        print(f"bf16 grad {name}: rel {rel:.4f}")
-    assert worst < 0.25, worst  # measured 0.150 (layer-0 weights); a mis-ordered row gives > 1
+        rel, rel_ac = _rel_l2(v, g[key]), _rel_l2(b[key], g[key])
+        rep[name] = (round(rel, 4), round(rel_ac, 4))
+        assert rel <= max(BF16_FLOOR, BF16_VS_AUTOCAST * rel_ac), (name, rel, rel_ac)
+    print(f"bf16 grads (ours, reference autocast) rel L2: {rep}")
+    write_report("bf16_vs_autocast", "mlp_lego", dict(per_tensor=rep, worst_ratio=max(a / max(c, 1e-12) for a, c in
+                                                                                        rep.values())))
 
 
 @pytest.mark.parametrize("precision", ["fp32", "fp32x3", "bf16"])
@@ -209,7 +237,7 @@ def test_conditional_mlp_global_codes(pkg, golden, precision):
                 ref = g[f"gradval:{name}"]
                 close(v.reshape(-1)[g[f"gradidx:{name}"]], ref, 1e-5 * max(1.0, np.abs(ref).max()), 1e-4)
     else:
-        assert np.linalg.norm(n(codes.grad) - gref) <= 0.25 * np.linalg.norm(gref)
+        assert np.linalg.norm(n(codes.grad) - gref) <= bf16_grad_bound(golden) * np.linalg.norm(gref)
     with pytest.raises(ValueError):
         m(t(g["origins"]), t(g["directions"]), t(g["lengths"]), global_codes=t(np.zeros((3, 1, 3), np.float32)))
     with pytest.raises(ValueError):
@@ -810,12 +838,13 @@ def test_lego256_two_pass_vs_oracle(pkg, precision):
 
 
 @pytest.mark.parametrize("precision", FP32_MODES + ["bf16"])
-def test_lego256_mlp_gradients_vs_oracle(pkg, precision):
+def test_lego256_mlp_gradients_vs_oracle(pkg, golden, precision):
     """NeRFMLP forward + backward at 320 points per ray (32 rays, 10,240 points) against the oracle's backward.
     At this many points a few pre-activations sit within round-off of zero and flip their ReLU mask between the GPU
     and the oracle; such a point changes its whole gradient row, so the gate is per tensor: relative L2 error
     <= 5e-3 (measured <= 1.4e-3; heads ~1e-6) and no element off by more than 2e-2 x the tensor's max (measured
-    <= 5.6e-3) in the fp32 modes, 0.25 relative L2 in bf16 (measured <= 0.13). A layout error gives O(1)."""
+    <= 5.6e-3) in the fp32 modes; in bf16 the reference's own bf16 error bound (bf16_grad_bound: 2 x its autocast
+    error, 0.258; measured <= 0.13). A layout error gives O(1)."""
     rng = np.random.default_rng(7)
     R, P = 32, 320
     o = (rng.standard_normal((R, 3)) * 0.3 + [0, 0, 4]).astype(np.float32)
@@ -834,7 +863,7 @@ def test_lego256_mlp_gradients_vs_oracle(pkg, precision):
         rel = np.linalg.norm(v - r) / max(np.linalg.norm(r), 1e-12)
         print(f"{precision} grad {name}: rel L2 {rel:.2e}, max {np.abs(v - r).max() / np.abs(r).max():.2e} of max")
         if precision == "bf16":
-            assert rel <= 0.25, name  # as test_mlp_bf16_gradients_elementwise
+            assert rel <= bf16_grad_bound(golden), name  # the reference's own bf16 error x BF16_VS_AUTOCAST
         else:
             assert rel <= 5e-3, name
             assert np.abs(v - r).max() <= 2e-2 * np.abs(r).max(), name
@@ -846,11 +875,11 @@ def test_lego256_mlp_gradients_vs_oracle(pkg, precision):
 
 @pytest.mark.parametrize("precision", FP32_MODES + ["bf16"])
 @pytest.mark.parametrize("R,P", [(37, 100), (19, 64), (5, 200), (3, 50), (17, 65)])
-def test_colour_direction_gradient_ragged(pkg, precision, R, P):
+def test_colour_direction_gradient_ragged(pkg, golden, precision, R, P):
     """The colour layer's direction columns, which the fp32 backward sums by rays (dZc summed per ray, times the
     ray's dirPE) once P >= 64, at ray counts and lengths that leave partial ray blocks, rays straddling two and three
     dZc chunks, and P below the chunk (the per-point dW tile then), against the oracle: relative L2 <= 1e-4 in the
-    fp32 modes on the rows without a ReLU flip (below), 0.25 in bf16 as test_lego256_mlp_gradients_vs_oracle (its
+    fp32 modes on the rows without a ReLU flip (below), bf16_grad_bound in bf16 as test_lego256_mlp_gradients_vs_oracle (its
     per-point tile reads the fp8-stored dZc: measured 0.051 at R, P = 37, 100). A wrong chunk slot or ray gives O(1)."""
     rng = np.random.default_rng(R * 1000 + P)
     o = (rng.standard_normal((R, 3)) * 0.3 + [0, 0, 4]).astype(np.float32)
@@ -873,7 +902,7 @@ def test_colour_direction_gradient_ragged(pkg, precision, R, P):
         rel[key] = np.linalg.norm(w[:, cols] - r[:, cols]) / np.linalg.norm(r[:, cols])
         print(f"{precision} R={R} P={P} colour {key} columns: rel L2 {rel[key]:.2e}")
     if precision == "bf16":
-        assert rel["dir"] <= 0.25, rel
+        assert rel["dir"] <= bf16_grad_bound(golden), rel
         return
     assert rel["dir"] <= 5e-3, rel
     # a colour unit whose pre-activation sits within round-off of zero at some point flips its ReLU between the GPU

@@ -268,6 +268,51 @@ def test_trainer_trajectory_matches_reference(golden, precision):
     assert ok, report
 
 
+BF16_VS_AUTOCAST = 2.0  # as tests/test_gpu_parity.py: bf16 bounded by the reference's own bf16 error, x2
+
+
+def test_trainer_trajectory_bf16_within_the_references_own_bf16(golden):
+    """The bf16 throughput mode over the same 20-step trajectory (train_trajectory.npz's draws injected, its own
+    refinement), against the reference's OWN bf16 trajectory (train_trajectory_bf16ref.npz: the reference's 20 steps on
+    the same draws under torch.autocast("cpu", bfloat16)): every step's objective within BF16_VS_AUTOCAST x the
+    autocast run's largest distance from the fp32 reference's objective, and per model the parameter change after the
+    20 steps no further from the exact (float64) trajectory's than BF16_VS_AUTOCAST x the autocast run's, in relative L2
+    and in max norm."""
+    from yanerf_amd import ops
+    g, gb = golden("train_trajectory"), golden("train_trajectory_bf16ref")
+    R, hw, K = int(g["n_rays"]), int(g["hw"]), int(g["steps"])
+    tr = make_trainer("bf16", g["seeds"], n_rays=R, hw=hw, runner_cfg=lego_cfg().runner)
+    focal = t(g["focal"])
+    losses = []
+    for k in range(K):
+        draws = dict(pixel_ids=t(g[f"pixel_ids:{k}"], torch.int64), jitter_u=t(g[f"jitter_u:{k}"]),
+                     noise=[t(g[f"noise_coarse:{k}"]), t(g[f"noise_fine:{k}"])], pdf_u=t(g[f"pdf_u:{k}"]))
+        with ops.injected_randomness(**draws):
+            out = tr.step(t(g["poses"][k:k + 1]), focal, t(g["images"][k:k + 1]))
+        losses.append(float((out["sq_fine"].sum() + out["sq_coarse"].sum()) / (R * 3)))
+    torch.cuda.synchronize()
+    ours_err = np.abs(np.array(losses) - g["losses"][:, 0])
+    ac_err = np.abs(gb["losses"][:, 0] - g["losses"][:, 0])
+    report = dict(steps=K, max_objective_err_vs_reference=float(ours_err.max()),
+                  autocast_max_objective_err_vs_reference=float(ac_err.max()))
+    ok = ours_err.max() <= BF16_VS_AUTOCAST * ac_err.max()
+    deltas = _trajectory_deltas(g, tr)
+    for i, (m, p0) in enumerate(zip(tr.models, model_params(g["seeds"]))):
+        key = "coarse" if i == 0 else "fine"
+        ac = np.concatenate([gb[f"param{i}:{name}"].astype(np.float64).reshape(-1) - p0[name].astype(np.float64).reshape(
+            -1)[g[f"paramidx{i}:{name}"] if f"paramidx{i}:{name}" in g else slice(None)]
+            for name, _ in m.named_parameters()])
+        ours, _, ex = deltas[key]
+        l2 = lambda x: float(np.linalg.norm(x - ex) / np.linalg.norm(ex))  # noqa: E731
+        mx = lambda x: float(np.abs(x - ex).max() / np.abs(ex).max())  # noqa: E731
+        report.update({f"{key}_ours_vs_exact_l2": l2(ours), f"{key}_autocast_vs_exact_l2": l2(ac),
+                       f"{key}_ours_vs_exact_max": mx(ours), f"{key}_autocast_vs_exact_max": mx(ac)})
+        ok &= l2(ours) <= BF16_VS_AUTOCAST * l2(ac) and mx(ours) <= BF16_VS_AUTOCAST * mx(ac)
+    print(f"bf16 trajectory vs the reference's own bf16: {report}")
+    write_report("train_trajectory", "bf16 vs reference autocast", report)
+    assert ok, report
+
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_trainer_step_matches_registry_step(golden, precision):
     """The fused step and the drop-in registry path (NeRFPipeline + autograd) on the same injected draws: same kernels,
@@ -527,7 +572,7 @@ def tr_coarse_weights(tr, g, H, W, hw=800):
 
 
 @pytest.mark.parametrize("precision", ["fp32", "fp32x3"])
-def test_full_image_800_vs_oracle(precision):
+def test_full_image_800_vs_oracle(golden, precision):
     """BASELINE configs[1] at full size: one whole 800 x 800 Lego evaluation image (64 + 128 samples, 640,000 rays)
     through the fused path (NeRFTrainer.render) and through the drop-in registry pipeline (313 chunks of 131,072
     points, as nerf_pipeline.py:217-236 chunks it). 2,048 rays on a stride across the image are rendered by the CPU
@@ -572,6 +617,20 @@ def test_full_image_800_vs_oracle(precision):
     split_gate(n(f).reshape(-1, 3)[idx], ref["fine"][0], z_gpu, ref["z_fine"], n(d).reshape(-1)[idx],
                ref["fine"][1].reshape(-1), fine_at=fine_at, tag=f"800x800 {precision}",
                coarse=(O, z, n(ro.prev_stage.aux["weights"]), 128))
+    # ... and against the REFERENCE's own render of the same rays (sensitivity_lego_800.npz, make_golden.gen_sensitivity:
+    # its two-pass evaluation render of these 2,048 rays with the ulp / float64 / hip-arithmetic trials): coarse stage
+    # strict, fine stage through the split gate with set membership in the reference's own sensitive set, and in fp32
+    # the coarse weights equal to the reference's pipeline run in this build's arithmetic, bit for bit
+    sens = golden("sensitivity_lego_800")
+    assert np.array_equal(sens["subset"], idx)
+    w_ours = n(ro.prev_stage.aux["weights"]).reshape(S, 64)
+    np.testing.assert_allclose(w_ours, sens["base_coarse_weights"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(n(c).reshape(-1, 3)[idx], sens["base_coarse_features"], atol=1e-5, rtol=0)
+    if precision == "fp32":
+        np.testing.assert_array_equal(w_ours, sens["hip_arithmetic_coarse_weights"].reshape(S, 64))
+    split_gate(n(f).reshape(-1, 3)[idx], sens["base_fine_features"], z_gpu, sens["base_z_fine"], n(d).reshape(-1)[idx],
+               sens["base_fine_depths"], fine_at=fine_at, tag=f"800x800 {precision} vs reference",
+               coarse=(O, z, w_ours, 128), sensitivity=sens, hip_exact=precision == "fp32")
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])

@@ -34,7 +34,7 @@ EXPORTS = (
     "yanerf_last_error", "yanerf_version", "yanerf_build_id", "yanerf_raygen", "yanerf_mlp_num_params",
     "yanerf_mlp_packed_bytes",
     "yanerf_mlp_pack", "yanerf_mlp_pack_multi", "yanerf_mlp_saved_bytes", "yanerf_mlp_bwd_workspace_bytes",
-    "yanerf_mlp_forward",
+    "yanerf_mlp_dw_plan", "yanerf_mlp_forward",
     "yanerf_mlp_backward", "yanerf_mlp_backward_phase", "yanerf_composite_forward", "yanerf_composite_backward",
     "yanerf_composite_train", "yanerf_sample_pdf",
     "yanerf_refine", "yanerf_rgb_loss", "yanerf_adam", "yanerf_adam_scalars", "yanerf_adam_table", "yanerf_step_advance",
@@ -91,6 +91,8 @@ def lib():
         "yanerf_mlp_pack_multi": (c_int, [c_int, POINTER(MlpDesc), c_int, P, P, P]),
         "yanerf_mlp_saved_bytes": (i64, [POINTER(MlpDesc), c_int, i64]),
         "yanerf_mlp_bwd_workspace_bytes": (i64, [POINTER(MlpDesc), c_int, i64]),
+        "yanerf_mlp_dw_plan": (c_int, [POINTER(MlpDesc), c_int, i64, POINTER(c_int), POINTER(c_int), POINTER(i64),
+                                       POINTER(i64), POINTER(i64)]),
         "yanerf_mlp_forward": (c_int, [POINTER(MlpDesc), c_int, P, P, P, P, i64, i64, P, P, P, P]),
         "yanerf_mlp_backward": (c_int, [POINTER(MlpDesc), c_int, P, P, P, P, P, i64, i64, P, P, P]),
         "yanerf_mlp_backward_phase": (c_int, [POINTER(MlpDesc), c_int, P, P, P, P, P, i64, i64, P, P, c_int, P]),
@@ -125,6 +127,17 @@ def check(status: int, what: str) -> None:
     if status != 0:
         msg = lib().yanerf_last_error().decode(errors="replace")
         raise HipError(f"{what} failed: {msg}")
+
+
+def dw_plan(desc: MlpDesc, precision: int, n_points: int) -> dict:
+    """The split-K weight-gradient plan for n_points (yanerf_mlp_dw_plan): tiles, splits, points per stage and the
+    stages per split."""
+    t, s = c_int(), c_int()
+    sp, lo, hi = c_int64(), c_int64(), c_int64()
+    check(lib().yanerf_mlp_dw_plan(ctypes.byref(desc), precision, int(n_points), ctypes.byref(t), ctypes.byref(s),
+                                   ctypes.byref(sp), ctypes.byref(lo), ctypes.byref(hi)), "yanerf_mlp_dw_plan")
+    return dict(tiles=t.value, splits=s.value, stage_points=sp.value, stages_per_split=[lo.value, hi.value],
+                points_per_split=[lo.value * sp.value, hi.value * sp.value])
 
 
 def ptr_array(ptrs):

@@ -3228,6 +3228,25 @@ int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, 
   return grad_bytes + (int64_t)S * se * 4 + (2 * (Npad / CH) * HC + nblk * HC * KDIR) * 4;
 }
 
+int yanerf_mlp_dw_plan(const yanerf_mlp_desc* d, int precision, int64_t n_points, int* tiles, int* splits,
+                       int64_t* stage_points, int64_t* stages_min, int64_t* stages_max) {
+  if (check_desc(d)) return 1;
+  YN_CHECK(n_points >= 0, "mlp_dw_plan: bad n_points %lld", (long long)n_points);
+  YN_CHECK(tiles && splits && stage_points && stages_min && stages_max, "mlp_dw_plan: null pointer");
+  const MlpLayout L = make_layout(d, precision);
+  const int64_t Npad = npad_of(precision, n_points);
+  int t = 0;
+  dw_slab_elems_for(L, precision, &t);
+  const int64_t nst = Npad / dw_stage_pts(precision);
+  const int S = dw_splits(t, nst, prec_pm(precision));
+  *tiles = t;
+  *splits = S;
+  *stage_points = dw_stage_pts(precision);
+  *stages_min = nst / S;  // split s covers stages [nst s / S, nst (s + 1) / S) (dw tile kernels)
+  *stages_max = (nst + S - 1) / S;
+  return 0;
+}
+
 int yanerf_mlp_forward(const yanerf_mlp_desc* d, int precision, const void* packed, const float* origins,
                        const float* directions, const float* lengths, int64_t R, int64_t P, float* sigma_raw,
                        float* rgb, void* saved, void* stream) {

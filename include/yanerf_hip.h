@@ -238,11 +238,13 @@ int yanerf_adam(float* params, const float* grads, float* exp_avg, float* exp_av
 int yanerf_adam_scalars(double lr, double beta1, double beta2, int64_t step, float* out2);
 /* yanerf_adam with the step's scalars read on the device: row *index of table [K][2] (filled with
  * yanerf_adam_scalars), so a captured step (hipGraph) replays with each step's learning rate and bias corrections.
- * Bit-identical to yanerf_adam with the same scalars. Not a reference entry point (scripts/run.py:158-160's
- * torch.optim.Adam, as yanerf_adam). */
-int yanerf_adam_table(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+ * Bit-identical to yanerf_adam with the same scalars. avg_over > 1: `grads` holds the SUM over that many
+ * data-parallel ranks and is first averaged in place (grads / avg_over, the division DDP applies after its
+ * all-reduce, run.py:162-166); 1 = as given. Not a reference entry point (scripts/run.py:158-160's torch.optim.Adam,
+ * as yanerf_adam). */
+int yanerf_adam_table(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                       const float* table, const int64_t* index, double beta1, double beta2, double eps,
-                      double weight_decay, void* stream);
+                      double weight_decay, int64_t avg_over, void* stream);
 /* The device-side step state of a graph-capturable training step: state[0] (the Philox offset base read through the
  * rng_base pointers of yanerf_raygen / yanerf_refine / yanerf_raymarch_opts) += rng_delta, state[1] (the Adam table
  * index) += 1. One thread, stream-ordered. */

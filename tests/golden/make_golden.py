@@ -1216,16 +1216,27 @@ def gen_train_step_lego_4096(out):
         reference-derived bound);
       * the oracle under the reference's own ReLU decisions (O_ref of parity_gates.tie_budget_gate, in 512-ray chunks
         whose gradients add up) with each element's sum of |terms|, pinned here to the reference's gradients."""
+    out["train_step_lego_4096"] = _full_step(128, (81, 82), (15.0, -35.0), 18, 19, relu_oracle=True)
+
+
+def gen_train_step_lego256_4096(out):
+    """BASELINE configs[4]'s training step (Lego, 64 + 256 samples: 320 fine points per ray, 1.31 M fine points) at its
+    full 4096 rays through the reference, as gen_train_step_lego_4096 without the ReLU record and the oracle: the draws,
+    depths, per-ray outputs, objective and gradients, and the float64 and bf16-autocast re-runs on the same draws and
+    depths. The bf16 mode's weight gradients then run two rounds of splits (yanerf_mlp_dw_plan: 36 splits)."""
+    out["train_step_lego256_4096"] = _full_step(256, (91, 92), (-40.0, -25.0), 28, 29, relu_oracle=False)
+
+
+def _full_step(n_fine, seeds, view, img_seed, torch_seed, relu_oracle):
     sys.path.insert(0, str(HERE.parents[1]))
     from oracle import nerf_oracle as O
     R = FULL_RAYS
-    pcfg = lego_pipeline_cfg()
+    pcfg = lego_pipeline_cfg(n_fine=n_fine)
     assert int(pcfg.ray_sampler.n_rays_per_image_sampled_from_mask) == R
-    seeds = (81, 82)
-    pose = torch.from_numpy(synthetic_pose(15.0, -35.0, 4.0))[None]
+    pose = torch.from_numpy(synthetic_pose(view[0], view[1], 4.0))[None]
     focal = torch.tensor([1111.1111])
-    img = torch.rand(1, 800, 800, 3, generator=torch.Generator().manual_seed(18))
-    Pc, Pf = 64, 192
+    img = torch.rand(1, 800, 800, 3, generator=torch.Generator().manual_seed(img_seed))
+    Pc, Pf = 64, 64 + n_fine
 
     def build(dtype=torch.float32):
         pipe = PIPELINES.build(pcfg)
@@ -1247,7 +1258,7 @@ def gen_train_step_lego_4096(out):
 
     masks, cands, hashes, stage_out = {}, {}, {}, []
     hooks = [pipe.renderer.register_forward_hook(lambda m, i, o: stage_out.append(o))]
-    for k, f in enumerate(pipe.implicit_functions):
+    for k, f in enumerate(pipe.implicit_functions if relu_oracle else []):
         mods = [(li, layer[1]) for li, layer in enumerate(f._fn.xyz_encoder.mlp)] + [(8, f._fn.color_layer[1])]
         for li, mod in mods:
             def hook(m, inp, k=k, li=li):  # a PRE-hook: the reference's ReLUs are in place
@@ -1262,7 +1273,7 @@ def gen_train_step_lego_4096(out):
                     np.float32))
             hooks.append(mod.register_forward_pre_hook(hook))
     RayPointRefiner.forward = rec_fwd
-    torch.manual_seed(19)
+    torch.manual_seed(torch_seed)
     try:
         with rec.capture():
             preds = pipe(poses=pose, focal_lengths=focal, image_rgb=img, evaluation_mode=EvaluationMode.TRAINING)
@@ -1282,7 +1293,7 @@ def gen_train_step_lego_4096(out):
              noise_fine=np32(rec.log[4][1]), coarse_weights=np32(refined[0][0]).reshape(R, Pc), z_fine=z_fine,
              coarse_features=np32(coarse_o.features).reshape(R, 3), coarse_depths=np32(coarse_o.depths).reshape(R),
              fine_features=np32(fine_o.features).reshape(R, 3), fine_depths=np32(fine_o.depths).reshape(R),
-             tie_rel=np.float32(FULL_TIE_REL))
+             **({"tie_rel": np.float32(FULL_TIE_REL)} if relu_oracle else {}))
     for kk in ("objective", "loss_rgb_mse", "loss_prev_stage_rgb_mse"):
         d[kk] = np32(preds[kk])
     for (k, li), hsh in hashes.items():
@@ -1349,10 +1360,12 @@ def gen_train_step_lego_4096(out):
     del pbf
     print("train_step_lego_4096: bf16 autocast re-run", flush=True)
 
+    if not relu_oracle:
+        return d
     # ---- the oracle under the reference's own ReLU decisions at its depths (O_ref), in 512-ray chunks
     arch = O.MLPArch.from_dict(LEGO_ARCH)
     pc, pf = make_nerf_mlp_params(LEGO_ARCH, seeds[0]), make_nerf_mlp_params(LEGO_ARCH, seeds[1])
-    cfg = O.RenderCfg(n_pts_fine=128, density_noise_std=0.2, raymarch=O.RaymarchOpts(background_density_bias=1e-6))
+    cfg = O.RenderCfg(n_pts_fine=n_fine, density_noise_std=0.2, raymarch=O.RaymarchOpts(background_density_bias=1e-6))
     o, dd, z, _ = O.sample_rays_train(d["pose"], d["focal"], 800, 800, 2.0, 6.0, Pc, ids, d["jitter_u"])
     o, dd, z = o.reshape(R, 3), dd.reshape(R, 3), z.reshape(R, Pc)
     nc = (d["noise_coarse"].reshape(R, Pc) * np.float32(0.2)).astype(np.float32)
@@ -1389,14 +1402,14 @@ def gen_train_step_lego_4096(out):
             pin = max(pin, float(err.max() / M))
     d["oracle_pin_max"] = np.float64(pin)
     print(f"train_step_lego_4096: oracle pinned to the reference at {pin:.3e} x max", flush=True)
-    out["train_step_lego_4096"] = d
+    return d
 
 
 GENERATORS = (gen_harmonic, gen_raysampler, gen_mlp, gen_raymarcher, gen_sample_pdf, gen_render_eval,
               gen_train_step, gen_zero_outputer, gen_init_checksums, gen_pipeline_state, gen_lr_schedule,
               gen_raysampler_masked, gen_iter_runner, gen_render_fern, gen_train_step_fern, gen_sensitivity,
               gen_render_trained, gen_train_step_trained, gen_train_trajectory, gen_train_step_lego_4096,
-              gen_mlp_bf16ref, gen_train_trajectory_bf16ref)
+              gen_mlp_bf16ref, gen_train_trajectory_bf16ref, gen_train_step_lego256_4096)
 
 
 def main():

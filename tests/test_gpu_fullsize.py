@@ -53,10 +53,16 @@ def g4096(golden):
     return golden("train_step_lego_4096")
 
 
-def lego_cfg():
+def lego_cfg(n_fine=128):
     import yanerf_boot
     from yanerf_amd.utils.config import Config
-    return Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml"))
+    cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml"))
+    cfg.pipeline.renderer.n_pts_per_ray_fine_training = cfg.pipeline.renderer.n_pts_per_ray_fine_evaluation = n_fine
+    return cfg
+
+
+def n_fine_of(g):
+    return int(g["z_fine"].shape[-1]) - PC
 
 
 def params_of(g):
@@ -85,8 +91,8 @@ def target_image(g):
 def run_trainer(g, precision):
     from yanerf_amd import ops
     from yanerf_amd.train import NeRFTrainer
-    tr = NeRFTrainer(lego_cfg().pipeline, precision=precision, device=DEV)
-    assert tr.R == R and tr.Pc == PC and tr.Pf == PF  # lego.yml as written: configs[1]
+    tr = NeRFTrainer(lego_cfg(n_fine_of(g)).pipeline, precision=precision, device=DEV)
+    assert tr.R == R and tr.Pc == PC and tr.Pf == PC + n_fine_of(g)  # lego.yml (configs[1]; configs[4]: 64 + 256)
     tr.load_pipeline_state_dict(state_of(g))
     with ops.injected_randomness(**draws_of(g)):
         out = tr.step(t(g["pose"]), t(g["focal"]), target_image(g))
@@ -94,10 +100,10 @@ def run_trainer(g, precision):
     return tr, out
 
 
-def dw_plans(spec):
+def dw_plans(spec, pf=PF):
     from yanerf_amd import _C
     return {"coarse": _C.dw_plan(spec.desc(), spec.precision, R * PC), "fine": _C.dw_plan(spec.desc(), spec.precision,
-                                                                                         R * PF)}
+                                                                                         R * pf)}
 
 
 # ------------------------------------------------------------------------------------------- ReLU decisions
@@ -305,16 +311,13 @@ def rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-def test_full_size_bf16_step_within_the_references_own_bf16_error(g4096):
-    """bf16 at full size (the multi-split fp8 dW path, yanerf_mlp_dw_plan in the report): per gradient tensor, the
-    relative L2 error of our bf16 gradients against the reference's fp32 ones is at most BF16_VS_AUTOCAST x the
-    reference's own bf16 error (torch.autocast("cpu", bfloat16) on the same draws and depths), or within BF16_FLOOR;
-    the objective within the autocast objective's own distance x 2 (or 1e-3)."""
-    g = g4096
+def bf16_vs_autocast(g, tag):
+    """Our bf16 step on the golden's draws and depths against the reference's fp32 and bf16-autocast gradients."""
     tr, out = run_trainer(g, "bf16")
     obj = float((out["sq_fine"].sum() + out["sq_coarse"].sum()) / (R * 3))
     ref_obj, ac_obj = float(g["objective"][0]), float(g["objective_bf16ac"])
-    rep = dict(dw_plan=dw_plans(tr.specs[1]), objective_err=abs(obj - ref_obj), autocast_objective_err=abs(ac_obj - ref_obj))
+    rep = dict(dw_plan=dw_plans(tr.specs[1], tr.Pf), objective_err=abs(obj - ref_obj),
+               autocast_objective_err=abs(ac_obj - ref_obj))
     ratios, per = {}, {}
     for i, name, v, ref, idx in golden_grad_items(g, tr.models):
         ac = g[f"grad_bf16ac{i}:{name}"] if idx is None else g[f"grad_bf16acval{i}:{name}"]
@@ -325,8 +328,44 @@ def test_full_size_bf16_step_within_the_references_own_bf16_error(g4096):
     rep["worst_ratio"] = max(ratios.values())
     rep["worst_ours_rel_l2"] = max(v[0] for v in per.values())
     rep["worst_autocast_rel_l2"] = max(v[1] for v in per.values())
-    print(f"full-size bf16 step: {rep}")
-    write_report("train_step_4096", "trainer bf16 vs reference autocast", rep)
+    print(f"full-size bf16 step {tag}: {rep}")
+    write_report("train_step_4096", f"{tag} trainer bf16 vs reference autocast", rep)
     assert rep["objective_err"] <= max(1e-3, 2 * rep["autocast_objective_err"]), rep
     for k, (e_ours, e_ac) in per.items():
         assert e_ours <= max(BF16_FLOOR, BF16_VS_AUTOCAST * e_ac), (k, e_ours, e_ac)
+
+
+def test_full_size_bf16_step_within_the_references_own_bf16_error(g4096):
+    """bf16 at full size (the multi-split fp8 dW path, yanerf_mlp_dw_plan in the report): per gradient tensor, the
+    relative L2 error of our bf16 gradients against the reference's fp32 ones is at most BF16_VS_AUTOCAST x the
+    reference's own bf16 error (torch.autocast("cpu", bfloat16) on the same draws and depths), or within BF16_FLOOR;
+    the objective within the autocast objective's own distance x 2 (or 1e-3)."""
+    bf16_vs_autocast(g4096, "configs[1]")
+
+
+@pytest.fixture(scope="module")
+def g4096_256(golden):
+    return golden("train_step_lego256_4096")
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3", "bf16"])
+def test_configs4_full_size_step_matches_reference(g4096_256, precision):
+    """BASELINE configs[4]'s step (Lego, 64 + 256 samples: 4096 rays x 384 points, 1.31 M fine points) at full size
+    against the reference's own step (train_step_lego256_4096.npz): the fp32 modes by the objective (1e-6), the per-ray
+    outputs and the float64 yardstick; bf16 (the mode configs[4] names, here bf16 + fp8 storage; its weight gradients in
+    two rounds of 18 splits) within BF16_VS_AUTOCAST x the reference's own bf16-autocast error per gradient tensor."""
+    g = g4096_256
+    if precision == "bf16":
+        bf16_vs_autocast(g, "configs[4]")
+        return
+    tr, out = run_trainer(g, precision)
+    obj = float((out["sq_fine"].sum() + out["sq_coarse"].sum()) / (R * 3))
+    rep = dict(precision=precision, dw_plan=dw_plans(tr.specs[1], tr.Pf),
+               objective_err=abs(obj - float(g["objective"][0])))
+    assert rep["objective_err"] <= 1e-6, rep
+    assert np.abs(n(tr.passes[0].w) - g["coarse_weights"]).max() <= 1e-5
+    np.testing.assert_allclose(n(tr.passes[1].feats), g["fine_features"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(n(tr.passes[1].depth), g["fine_depths"], atol=1e-4, rtol=0)
+    rep.update(exact_report(g, tr.models, f"configs[4] {precision}"))
+    print(f"configs[4] full-size step {precision}: {rep}")
+    write_report("train_step_4096", f"configs[4] trainer {precision} depths=reference", rep)

@@ -107,7 +107,7 @@ def lib():
         "yanerf_scatter_rays": (c_int, [P, P, i64, i64, i64, i64, i64, P, P, P, P]),
         "yanerf_adam": (c_int, [P, P, P, P, i64, c_double, c_double, c_double, c_double, c_double, i64, P]),
         "yanerf_adam_scalars": (c_int, [c_double, c_double, c_double, i64, POINTER(c_float)]),
-        "yanerf_adam_table": (c_int, [P, P, P, P, i64, P, P, c_double, c_double, c_double, c_double, P]),
+        "yanerf_adam_table": (c_int, [P, P, P, P, i64, P, P, c_double, c_double, c_double, c_double, i64, P]),
         "yanerf_step_advance": (c_int, [P, c_uint64, P]),
     }
     for name, (res, args) in sig.items():

@@ -751,16 +751,22 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   p[i] = __fmaf_rn(neg_step_size, mi / denom, pi);        // _foreach_addcdiv_(params, exp_avgs, denom, -step_size)
 }
 // the same update with the step's two scalars read on the device from a per-step table (row *index): a graph-captured
-// step replays with the schedule's values of the step it runs as
-__global__ void adam_table_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+// step replays with the schedule's values of the step it runs as. grad_div != 1: the gradients are the sum over the
+// data-parallel ranks and are first averaged in place, g = g / world (the true division DDP's `div_` does,
+// run.py:162-166), so the exchange's divide costs no launch of its own
+__global__ void adam_table_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                   float* __restrict__ v, int64_t n, float w1, float b2, float w2, float eps, float wd,
-                                  const float* __restrict__ table, const int64_t* __restrict__ index) {
+                                  const float* __restrict__ table, const int64_t* __restrict__ index, float grad_div) {
   const int64_t k = *index;
   const float neg_step_size = table[2 * k], bc2_sqrt = table[2 * k + 1];
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float pi = p[i];
   float gi = g[i];
+  if (grad_div != 1.0f) {
+    gi = gi / grad_div;
+    g[i] = gi;
+  }
   if (wd != 0.0f) gi = __fmaf_rn(wd, pi, gi);
   const float mi = __fmaf_rn(w1, gi - m[i], m[i]);
   const float vi = __fmaf_rn(w2, gi * gi, v[i] * b2);
@@ -957,15 +963,16 @@ int yanerf_adam(float* params, const float* grads, float* exp_avg, float* exp_av
   return 0;
 }
 
-int yanerf_adam_table(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+int yanerf_adam_table(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                       const float* table, const int64_t* index, double beta1, double beta2, double eps,
-                      double weight_decay, void* stream) {
+                      double weight_decay, int64_t avg_over, void* stream) {
   YN_CHECK(n >= 0, "adam_table: negative size");
+  YN_CHECK(avg_over >= 1 && avg_over <= (1 << 24), "adam_table: avg_over %lld", (long long)avg_over);
   if (n == 0) return 0;
   YN_CHECK(params && grads && exp_avg && exp_avg_sq && table && index, "adam_table: null pointer");
   hipLaunchKernelGGL(adam_table_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), params,
                      grads, exp_avg, exp_avg_sq, n, (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
-                     (float)eps, (float)weight_decay, table, index);
+                     (float)eps, (float)weight_decay, table, index, (float)avg_over);
   YN_LAUNCH_CHECK("adam_table");
   return 0;
 }

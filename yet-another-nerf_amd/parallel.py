@@ -64,6 +64,14 @@ def allreduce_mean_(flat: torch.Tensor) -> torch.Tensor:
     return flat
 
 
+def allreduce_sum_(flat: torch.Tensor) -> torch.Tensor:
+    """In-place sum of a flat buffer over all ranks (the caller divides by the world size: NeRFTrainer does it inside
+    its Adam launch)."""
+    if is_dist():
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    return flat
+
+
 def allreduce_sum_async(t: torch.Tensor):
     """Start a sum all-reduce of `t` in place and return its handle (None without a process group). Under RCCL the
     collective runs on the process group's own stream after the work already queued on the current stream, so

@@ -403,6 +403,7 @@ class NeRFTrainer:
                     if self.exchange and self.grad_exchange == "bucketed":
                         self._h_early = parallel.allreduce_sum_async(self.flat.grad[:self.n_coarse])
         early = self._early()
+        avg_over = 1  # > 1: the flat gradient holds the sum over the ranks; Adam averages it in place (yanerf_adam_table)
         if self.exchange and not self.kernel_probes and self.grad_exchange == "bucketed":
             # Under data parallelism the gradient exchange is split in two buckets, one per model, overlapped with
             # the backward: the coarse MLP's backward runs first (or, "early", beside the fine forward on
@@ -422,7 +423,7 @@ class NeRFTrainer:
                 self._mlp_backward(1, st)
                 h2 = parallel.allreduce_sum_async(self.flat.grad[self.n_coarse:])
             self._probe("allreduce_exposed", lambda: (parallel.finish_allreduce(h), parallel.finish_allreduce(h2)))
-            self.flat.grad.div_(self.world)
+            avg_over = self.world  # DDP's divide by the world size, inside the Adam launch (no launch of its own)
         elif self.exchange and not self.kernel_probes:
             # "single": both backwards, then one all-reduce of the whole flat gradient (all of it exposed)
             self._mlp_backward(1, st)
@@ -430,7 +431,8 @@ class NeRFTrainer:
                 torch.cuda.current_stream().wait_stream(self.side)
             else:
                 self._mlp_backward(0, st)
-            self._probe("allreduce_exposed", lambda: parallel.allreduce_mean_(self.flat.grad))
+            self._probe("allreduce_exposed", lambda: parallel.allreduce_sum_(self.flat.grad))
+            avg_over = self.world
         elif self.kernel_probes:
             # timing probe mode (bench.py's per-kernel roofline): every MLP backward kernel alone on the stream, in the
             # order dX, dW, slab reduce; the result is identical to the other schedules
@@ -474,7 +476,7 @@ class NeRFTrainer:
         _C.check(L.yanerf_adam_table(_p(self.flat.data), _p(self.flat.grad), _p(self.exp_avg), _p(self.exp_avg_sq),
                                      self.flat.numel, _p(self._tab), ctypes.c_void_p(self._dstate.data_ptr() + 8),
                                      float(self.betas[0]), float(self.betas[1]), float(self.eps),
-                                     float(self.weight_decay), st), "yanerf_adam_table")
+                                     float(self.weight_decay), avg_over, st), "yanerf_adam_table")
         delta = self.rng.get_state()[1] - off0
         _C.check(L.yanerf_step_advance(rbase, delta, st), "yanerf_step_advance")
         if self._dstate_host is not None:

@@ -289,7 +289,7 @@ def test_full_size_registry_step_matches_reference(g4096, precision):
                      evaluation_mode=EvaluationMode.TRAINING)
     preds["objective"].mean().backward()
     torch.cuda.synchronize()
-    rep = dict(precision=precision, objective_err=abs(float(preds["objective"].mean()) - float(g["objective"][0])))
+    rep = dict(precision=precision, objective_err=abs(float(preds["objective"].detach().mean()) - float(g["objective"][0])))
     assert rep["objective_err"] <= 1e-6, rep
     models = [f._fn for f in pipe.implicit_functions]
     rep.update(exact_report(g, models, f"registry {precision}"))

@@ -343,10 +343,18 @@ def test_bench_two_ranks_one_card_reports_distributed_fields():
     """The real bench (fused training step, RCCL replaced by gloo because two ranks share the one card of a test box)
     under torch.distributed.run with 2 ranks: the N-rank line has the process group's backend and world size, both
     ranks' ms/step and the exposed gradient exchange (HIP events around the wait), and value = both ranks' rays / the
-    max-over-ranks time. Not a measurement (the ranks share one GPU)."""
-    from test_parallel import _run_bench_dist
-    d = _run_bench_dist(["--steps", "3", "--warmup", "1", "--psnr-steps", "0", "--secondary", "none", "--no-extras",
-                         "--no-cpu-baseline", "--rays", "1024"], timeout=600, env={"YANERF_DIST_BACKEND": "gloo"})
+    max-over-ranks time. Not a measurement (the ranks share one GPU). Launched as the driver launches it: the plain
+    `python bench.py --gpus 2`, which starts its two ranks itself (no torch.distributed.run on the command line)."""
+    import json
+
+    from test_parallel import _run_bench_plain
+    r = _run_bench_plain(["--gpus", "2", "--steps", "3", "--warmup", "1", "--psnr-steps", "0", "--secondary", "none",
+                          "--no-extras", "--no-cpu-baseline", "--rays", "1024"], timeout=600,
+                         env={"YANERF_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]  # rank 0 prints ONE JSON line
+    d = json.loads(lines[0])
     info = d["distributed"]
     assert d["n_gpus"] == 2 and info["backend"] == "gloo" and info["world_size"] == 2
     assert len(info["ms_per_step_per_rank"]) == 2 and all(v > 0 for v in info["ms_per_step_per_rank"])

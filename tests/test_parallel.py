@@ -146,13 +146,13 @@ def test_bench_distributed_fields_gloo_world2():
     assert info["selftest_grad_ok"]
 
 
-def _run_bench_plain(extra, timeout=300):
-    import json
+def _run_bench_plain(extra, timeout=300, env=None):
+    """`python bench.py EXTRA` with no launcher (and no launcher variables in the environment)."""
     import subprocess
     import sys
     from pathlib import Path
     root = Path(__file__).resolve().parents[1]
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env = dict({k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}, **(env or {}))
     r = subprocess.run([sys.executable, str(root / "bench.py")] + extra, capture_output=True, text=True,
                        timeout=timeout, env=env, cwd="/tmp")
     return r

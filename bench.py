@@ -80,7 +80,7 @@ MAC_PER_POINT = 589_952  # 63*256 + 4*256^2 + 319*256 + 2*256^2 + 2
 MAC_PER_RAY_PASS = 27 * 128  # LinearWithRepeat direction term, once per ray per pass
 # MI355X dense matrix peaks (MI355X_MICROARCH.md); fp32x3 runs six bf16 MFMAs per fp32 product, so its ceiling
 # for fp32 work is the bf16 peak / 6
-PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "fp32x3": 2500.0 / 6}
+PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "fp32x3": 2500.0 / 6, "bf16s": 2500.0}
 PEAK_FP8_TFLOPS = 5000.0  # block-scaled fp8 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, e4m3): 2x the bf16 rate, dense
 # The bf16 mode's weight-gradient kernel runs its fp8 x fp8 tiles (fp8 saved activations x fp8 gradient rows) on the
 # block-scaled fp8 MFMA and the rest (the bf16 PE / dirPE columns, the bf16 dU rows) on the bf16 MFMA. Algorithmic
@@ -333,39 +333,45 @@ def extras(pcfg, cfg, dev, poses, focal, image, precision, others=()):
     out["dropin_train"] = {"rays_per_s": round(R / dt, 1), "ms_per_step": round(1e3 * dt, 3), "precision": precision,
                            "path": "registry NeRFPipeline + autograd + torch.optim.Adam"}
     # BASELINE configs[4] on one GPU: bf16, 64 coarse + 256 fine samples (64 + 320 = 384 points per ray), the same
-    # fused training step (4096 rays), with its whole-step MFMA utilisation and the fine forward's roofline
+    # fused training step (4096 rays), with its whole-step MFMA utilisation and the fine forward's roofline -- in both
+    # bf16 storage modes: "bf16" (bf16 MFMA, fp8 e4m3 saved activations / gradient rows, dW on the fp8 MFMA; the
+    # top-level fields) and "bf16s" (bf16 storage throughout, dW on the bf16 MFMA: the precision configs[4] names)
     import copy as _copy
     c4 = _copy.deepcopy(pcfg)
     c4.renderer.n_pts_per_ray_fine_training = 256
     c4.renderer.n_pts_per_ray_fine_evaluation = 256
-    tr = NeRFTrainer(c4, precision="bf16", device=dev)
-    for i in range(3):
-        tr.step(poses[i:i + 1], focal, image)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    steps4 = 10
-    for i in range(steps4):
-        tr.step(poses[(3 + i) % len(poses)][None], focal, image)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps4
-    R4, Pc4, Pf4 = tr.R, tr.Pc, tr.Pf
-    # the fine forward timed alone on the GPU: a few steps in the trainer's probe mode (serial backward; bf16's
-    # default "early" schedule runs the coarse backward beside the fine forward in the steps timed above)
-    tr.kernel_probes = True
-    tr.enable_probes(["mlp_fwd_1"])
-    for i in range(3):
-        tr.step(poses[(13 + i) % len(poses)][None], focal, image)
-    torch.cuda.synchronize()
-    f4ms = tr.probe_ms().get("mlp_fwd_1", float("nan"))
-    tr.kernel_probes = False
-    tr.events = None
-    fwd4 = 2.0 * (MAC_PER_POINT * R4 * Pf4 + MAC_PER_RAY_PASS * R4)
+
+    def lego256(prec):
+        tr = NeRFTrainer(c4, precision=prec, device=dev)
+        for i in range(3):
+            tr.step(poses[i:i + 1], focal, image)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        steps4 = 10
+        for i in range(steps4):
+            tr.step(poses[(3 + i) % len(poses)][None], focal, image)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps4
+        R4, Pc4, Pf4 = tr.R, tr.Pc, tr.Pf
+        # the fine forward timed alone on the GPU: a few steps in the trainer's probe mode (serial backward; bf16's
+        # default "early" schedule runs the coarse backward beside the fine forward in the steps timed above)
+        tr.kernel_probes = True
+        tr.enable_probes(["mlp_fwd_1"])
+        for i in range(3):
+            tr.step(poses[(13 + i) % len(poses)][None], focal, image)
+        torch.cuda.synchronize()
+        f4ms = tr.probe_ms().get("mlp_fwd_1", float("nan"))
+        del tr
+        fwd4 = 2.0 * (MAC_PER_POINT * R4 * Pf4 + MAC_PER_RAY_PASS * R4)
+        return {"rays_per_s": round(R4 / dt, 1), "ms_per_step": round(1e3 * dt, 3), "pts_per_ray": Pc4 + Pf4,
+                "step_mfma_frac": round(train_flops_per_ray(Pc4, Pf4) * R4 / dt / 1e12 / PEAK_TFLOPS["bf16"], 4),
+                "fine_fwd_ms": round(f4ms, 4),
+                "fine_fwd_mfma_frac": round(fwd4 / (f4ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"], 4),
+                "dtype": DTYPES[prec]}
+
     out["lego256_bf16_train"] = {
         "config": "BASELINE configs[4] at 1 GPU: 64 coarse + 256 fine (64 + 320 fine-pass points), bf16",
-        "rays_per_s": round(R4 / dt, 1), "ms_per_step": round(1e3 * dt, 3), "pts_per_ray": Pc4 + Pf4,
-        "step_mfma_frac": round(train_flops_per_ray(Pc4, Pf4) * R4 / dt / 1e12 / PEAK_TFLOPS["bf16"], 4),
-        "fine_fwd_ms": round(f4ms, 4), "fine_fwd_mfma_frac": round(fwd4 / (f4ms * 1e-3) / 1e12 / PEAK_TFLOPS["bf16"], 4)}
-    del tr
+        **lego256("bf16"), "bf16s": lego256("bf16s")}
     # SURVEY §8(d)'s large-batch roofline variant: the same Lego 64 + 128 step at 16,384 and 65,536 rays per step (the
     # per-step fixed costs -- packs, ray generation, composites, refinement, reduces, Adam, launch gaps -- amortised
     # over 4-16x the MLP work), bf16's default schedule; fp32 at 16,384 rays
@@ -500,10 +506,16 @@ def configs_at_n(pcfg, cfg, dev, poses, focal, image, world: int, steps: int = 1
     c4 = _copy.deepcopy(pcfg)
     c4.renderer.n_pts_per_ray_fine_training = 256
     c4.renderer.n_pts_per_ray_fine_evaluation = 256
-    tr = NeRFTrainer(c4, precision="bf16", device=dev, runner_cfg=cfg.runner, train_set_size=LEGO_TRAIN_IMAGES)
     out["lego256_bf16_train"] = {"config": f"BASELINE configs[4] at {world} GPUs: Lego 800x800 bf16, 64 + 256, 4096 "
-                                           "rays per rank", **timed(tr, "bf16", poses, focal, image)}
-    del tr
+                                           "rays per rank"}
+    for p in ("bf16", "bf16s"):  # both bf16 storage modes (bf16s: bf16 throughout, the precision configs[4] names)
+        tr = NeRFTrainer(c4, precision=p, device=dev, runner_cfg=cfg.runner, train_set_size=LEGO_TRAIN_IMAGES)
+        r = timed(tr, p, poses, focal, image)
+        if p == "bf16":
+            out["lego256_bf16_train"].update(r)
+        else:
+            out["lego256_bf16_train"]["bf16s"] = r
+        del tr
     return out
 
 
@@ -580,7 +592,8 @@ def dist_selftest(steps: int) -> None:
 
 
 DTYPES = {"fp32": "f32", "fp32x3": "f32 (3xbf16 split MFMA)",
-          "bf16": "bf16 + fp8 (bf16 MFMA forward / dX; e4m3 saved activations and gradient rows; dW on the fp8 MFMA)"}
+          "bf16": "bf16 + fp8 (bf16 MFMA forward / dX; e4m3 saved activations and gradient rows; dW on the fp8 MFMA)",
+          "bf16s": "bf16 (bf16 MFMA forward / dX / dW; bf16 saved activations and gradient rows)"}
 LEGO_TRAIN_IMAGES = 100  # nerf_synthetic Lego's train split (the loader length scripts/run.py:243-271 converts with)
 GRAPH_STEPS = 4  # training steps captured per HIP graph in the graph legs (NeRFTrainer.capture_step(n_steps=...))
 
@@ -600,7 +613,7 @@ def main():
     ap.add_argument("--rays", type=int, default=None, help="rays per rank per step (default: config, 4096)")
     ap.add_argument("--config", default=str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--secondary", default="fp32x3,bf16",
+    ap.add_argument("--secondary", default="fp32x3,bf16,bf16s",
                     help="comma list of other precisions to time on the same workload (reported under `secondary`)")
     ap.add_argument("--no-extras", action="store_true", help="skip the eval-render and drop-in-path timings")
     ap.add_argument("--psnr-steps", type=int, default=1000,
@@ -719,7 +732,11 @@ def main():
         result["distributed"] = dist_info
     del tr
     # the other precision modes on the same workload, reported beside the headline (never in `value`)
-    notes = {"bf16": "throughput mode: bf16 weights/activations, fp32 accumulate; parity-gated only loosely",
+    notes = {"bf16": "throughput mode: bf16 weights/activations, fp32 accumulate, fp8 e4m3 storage of the saved "
+                     "activations / gradient rows; gradients within the reference's own bf16-autocast error "
+                     "(tests/test_gpu_fullsize.py)",
+             "bf16s": "bf16 with bf16 storage throughout (the precision of the reference under torch.autocast bf16); "
+                      "gradients within the reference's own bf16-autocast error (tests/test_gpu_fullsize.py)",
              "fp32x3": "fp32 operands as three bf16 planes, six bf16 MFMAs per product, fp32 saved "
                        "activations; passes the same strict parity gates as fp32 (tests/test_gpu_parity.py)",
              "fp32": "exact fp32 MFMA (v_mfma_f32_16x16x4_f32)"}

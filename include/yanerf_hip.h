@@ -38,6 +38,11 @@ extern "C" {
    2^-24 relative), fp32 accumulate, fp32 saved activations / gradients. fp32-class accuracy at ~2.6x the fp32
    MFMA rate. */
 #define YANERF_PREC_F32X3 2
+/* bf16 with bf16 storage throughout: the BF16 mode's kernels (bf16 MFMA forward and input-gradient walk, fp32
+   accumulate), but the saved activations and the gradient rows stay bf16 (no fp8 e4m3 sections) and the weight
+   gradients run on the bf16 MFMA over 32-point stages. The reference's own reduced precision (torch.autocast bf16 keeps
+   every Linear's operands bf16); YANERF_PREC_BF16 is the faster bf16 + fp8-storage mode. */
+#define YANERF_PREC_BF16S 3
 
 const char* yanerf_last_error(void);
 int yanerf_version(void);

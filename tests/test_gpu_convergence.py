@@ -92,7 +92,7 @@ def _target(H, W):
     return torch.from_numpy(img[None]).to(DEV)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp32x3", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3", "bf16", "bf16s"])
 def test_fused_trainer_converges(precision):
     import yanerf_boot  # noqa: F401
     from yanerf_amd.train import NeRFTrainer

@@ -33,7 +33,7 @@ def build(arch, precision, seed=3):
     return m
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp32x3"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp32x3", "bf16s"])
 def test_empty_bundle_through_the_mlp(ops, precision):
     """NeRFMLP.forward on a [1, 0, P] bundle: [1, 0, P, 1] densities and [1, 0, P, 3] colours, and a backward through
     them gives every parameter an all-zero gradient, as nn.Linear does on an empty batch."""

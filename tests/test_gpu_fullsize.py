@@ -311,9 +311,10 @@ def rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-def bf16_vs_autocast(g, tag):
-    """Our bf16 step on the golden's draws and depths against the reference's fp32 and bf16-autocast gradients."""
-    tr, out = run_trainer(g, "bf16")
+def bf16_vs_autocast(g, tag, precision="bf16"):
+    """Our bf16 step (bf16 + fp8 storage, or bf16s: bf16 storage throughout) on the golden's draws and depths against
+    the reference's fp32 and bf16-autocast gradients."""
+    tr, out = run_trainer(g, precision)
     obj = float((out["sq_fine"].sum() + out["sq_coarse"].sum()) / (R * 3))
     ref_obj, ac_obj = float(g["objective"][0]), float(g["objective_bf16ac"])
     rep = dict(dw_plan=dw_plans(tr.specs[1], tr.Pf), objective_err=abs(obj - ref_obj),
@@ -328,19 +329,20 @@ def bf16_vs_autocast(g, tag):
     rep["worst_ratio"] = max(ratios.values())
     rep["worst_ours_rel_l2"] = max(v[0] for v in per.values())
     rep["worst_autocast_rel_l2"] = max(v[1] for v in per.values())
-    print(f"full-size bf16 step {tag}: {rep}")
-    write_report("train_step_4096", f"{tag} trainer bf16 vs reference autocast", rep)
+    print(f"full-size {precision} step {tag}: {rep}")
+    write_report("train_step_4096", f"{tag} trainer {precision} vs reference autocast", rep)
     assert rep["objective_err"] <= max(1e-3, 2 * rep["autocast_objective_err"]), rep
     for k, (e_ours, e_ac) in per.items():
         assert e_ours <= max(BF16_FLOOR, BF16_VS_AUTOCAST * e_ac), (k, e_ours, e_ac)
 
 
-def test_full_size_bf16_step_within_the_references_own_bf16_error(g4096):
+@pytest.mark.parametrize("precision", ["bf16", "bf16s"])
+def test_full_size_bf16_step_within_the_references_own_bf16_error(g4096, precision):
     """bf16 at full size (the multi-split fp8 dW path, yanerf_mlp_dw_plan in the report): per gradient tensor, the
     relative L2 error of our bf16 gradients against the reference's fp32 ones is at most BF16_VS_AUTOCAST x the
     reference's own bf16 error (torch.autocast("cpu", bfloat16) on the same draws and depths), or within BF16_FLOOR;
     the objective within the autocast objective's own distance x 2 (or 1e-3)."""
-    bf16_vs_autocast(g4096, "configs[1]")
+    bf16_vs_autocast(g4096, "configs[1]", precision)
 
 
 @pytest.fixture(scope="module")
@@ -348,15 +350,15 @@ def g4096_256(golden):
     return golden("train_step_lego256_4096")
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp32x3", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3", "bf16", "bf16s"])
 def test_configs4_full_size_step_matches_reference(g4096_256, precision):
     """BASELINE configs[4]'s step (Lego, 64 + 256 samples: 4096 rays x 384 points, 1.31 M fine points) at full size
     against the reference's own step (train_step_lego256_4096.npz): the fp32 modes by the objective (1e-6), the per-ray
     outputs and the float64 yardstick; bf16 (the mode configs[4] names, here bf16 + fp8 storage; its weight gradients in
     two rounds of 18 splits) within BF16_VS_AUTOCAST x the reference's own bf16-autocast error per gradient tensor."""
     g = g4096_256
-    if precision == "bf16":
-        bf16_vs_autocast(g, "configs[4]")
+    if precision.startswith("bf16"):
+        bf16_vs_autocast(g, "configs[4]", precision)
         return
     tr, out = run_trainer(g, precision)
     obj = float((out["sq_fine"].sum() + out["sq_coarse"].sum()) / (R * 3))

@@ -153,16 +153,17 @@ def bf16_grad_bound(golden) -> float:
     return BF16_VS_AUTOCAST * worst
 
 
-def test_mlp_bf16_bounds(pkg, golden):
+@pytest.mark.parametrize("precision", ["bf16", "bf16s"])
+def test_mlp_bf16_bounds(pkg, golden, precision):
     """bf16 mode outputs on mlp_lego: RGB and sigma max error against the fp32 reference within BF16_VS_AUTOCAST x the
     reference's own autocast error (measured autocast: RGB 3.1e-3, sigma 5.3e-3), gradient norms within 10 %."""
     g, b = golden("mlp_lego"), golden("mlp_lego_bf16ref")
-    m, _ = build_mlp(pkg, LEGO_ARCH, int(g["seed"]), precision="bf16")
+    m, _ = build_mlp(pkg, LEGO_ARCH, int(g["seed"]), precision=precision)
     out = m(t(g["origins"]), t(g["directions"]), t(g["lengths"]))
     e = {k: float(np.abs(n(out[key]).reshape(-1) - g[k].reshape(-1)).max())
          for k, key in (("rgb", "rays_features"), ("sigma", "rays_densities"))}
     ac = {k: float(np.abs(b[k].reshape(-1) - g[k].reshape(-1)).max()) for k in ("rgb", "sigma")}
-    print(f"bf16 outputs: ours {e}, reference autocast {ac}")
+    print(f"{precision} outputs: ours {e}, reference autocast {ac}")
     for k in e:
         assert e[k] <= BF16_VS_AUTOCAST * ac[k], (k, e[k], ac[k])
     m.zero_grad()
@@ -173,14 +174,15 @@ def test_mlp_bf16_bounds(pkg, golden):
             close(np.linalg.norm(n(p.grad).astype(np.float64)), nn, 0.1 * nn)
 
 
-def test_mlp_bf16_gradients_elementwise(pkg, golden):
+@pytest.mark.parametrize("precision", ["bf16", "bf16s"])
+def test_mlp_bf16_gradients_elementwise(pkg, golden, precision):
     """bf16 mode, every parameter gradient element against the fp32 reference: relative L2 error per tensor (on the
     golden's full gradients, or its sampled elements for the large matrices) within BF16_VS_AUTOCAST x the reference's
     own autocast error on the same tensor (mlp_lego_bf16ref), or BF16_FLOOR (FP8_UNIT for the weights formed from an
     fp8-stored operand). Catches layout errors in the saved /
     gradient rows that the norm bound above would miss (a permuted row keeps the norm and gives > 1)."""
     g, b = golden("mlp_lego"), golden("mlp_lego_bf16ref")
-    m, _ = build_mlp(pkg, LEGO_ARCH, int(g["seed"]), precision="bf16")
+    m, _ = build_mlp(pkg, LEGO_ARCH, int(g["seed"]), precision=precision)
     out = m(t(g["origins"]), t(g["directions"]), t(g["lengths"]))
     m.zero_grad()
     ((out["rays_densities"] * t(g["g_sigma"])).sum() + (out["rays_features"] * t(g["g_rgb"])).sum()).backward()
@@ -192,14 +194,15 @@ def test_mlp_bf16_gradients_elementwise(pkg, golden):
             v = v.reshape(-1)[g[f"gradidx:{name}"]]
         rel, rel_ac = _rel_l2(v, g[key]), _rel_l2(b[key], g[key])
         rep[name] = (round(rel, 4), round(rel_ac, 4))
-        floor = max(BF16_FLOOR, FP8_UNIT if name in FP8_X_WEIGHTS else 0.0)
+        # the fp8-format floor applies to the fp8-storage mode only: bf16s stores these operands in bf16, as autocast
+        floor = max(BF16_FLOOR, FP8_UNIT if precision == "bf16" and name in FP8_X_WEIGHTS else 0.0)
         assert rel <= max(floor, BF16_VS_AUTOCAST * rel_ac), (name, rel, rel_ac)
     print(f"bf16 grads (ours, reference autocast) rel L2: {rep}")
-    write_report("bf16_vs_autocast", "mlp_lego", dict(per_tensor=rep, worst_ratio=max(a / max(c, 1e-12) for a, c in
+    write_report("bf16_vs_autocast", f"mlp_lego {precision}", dict(per_tensor=rep, worst_ratio=max(a / max(c, 1e-12) for a, c in
                                                                                         rep.values())))
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp32x3", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3", "bf16", "bf16s"])
 @pytest.mark.parametrize("R,P", [(4, 64), (3, 50), (1024, 64)])
 def test_density_bias_gradient_is_sum(pkg, precision, R, P):
     """d(sigma)/d(density bias) = 1, so its gradient is exactly sum(g_sigma) whatever the precision of the rest
@@ -216,11 +219,11 @@ def test_density_bias_gradient_is_sum(pkg, precision, R, P):
     exact = gs.double().sum().item()
     got = m.density_layer.bias.grad.double().item()
     # bf16 mode stores g_sigma in bf16 (relative rounding 2^-9 per element)
-    tol = 1e-5 if precision != "bf16" else 4e-3 * gs.abs().sum().item() / abs(exact)
+    tol = 1e-5 if not precision.startswith("bf16") else 4e-3 * gs.abs().sum().item() / abs(exact)
     assert abs(got - exact) <= tol * abs(exact), (got, exact)
 
 
-@pytest.mark.parametrize("precision", FP32_MODES + ["bf16"])
+@pytest.mark.parametrize("precision", FP32_MODES + ["bf16", "bf16s"])
 def test_conditional_mlp_global_codes(pkg, golden, precision):
     """latent_dim > 0 (reference tests/configs/pipelines/models/nerf_conditional_mlp.yml): each batch element's code
     is folded into layer 0's and the skip layer's bias; outputs, parameter and code gradients against the reference
@@ -231,7 +234,7 @@ def test_conditional_mlp_global_codes(pkg, golden, precision):
     codes = t(g["codes"]).requires_grad_(True)
     out = m(t(g["origins"]), t(g["directions"]), t(g["lengths"]), global_codes=codes)
     sig, rgb = out["rays_densities"], out["rays_features"]
-    strict = precision != "bf16"
+    strict = not precision.startswith("bf16")
     close(n(sig), g["sigma"], 2e-5 if strict else 5e-2, 1e-5 if strict else 5e-2)
     close(n(rgb), g["rgb"], 2e-6 if strict else 2e-2)
     m.zero_grad()
@@ -671,7 +674,7 @@ def test_chunking_invariance(pkg, golden):
     assert torch.equal(a, b) and torch.equal(a, c)
 
 
-@pytest.mark.parametrize("precision,n_fine", [("fp32", 128), ("fp32x3", 128), ("bf16", 128), ("bf16", 256)])
+@pytest.mark.parametrize("precision,n_fine", [("fp32", 128), ("fp32x3", 128), ("bf16", 128), ("bf16", 256), ("bf16s", 128), ("bf16s", 256)])
 def test_full_size_train_step_properties(pkg, precision, n_fine):
     """BASELINE configs[1]'s training step at its full size (Lego 800x800, 4096 rays, 64 + 128 samples, density noise),
     and configs[4]'s (bf16, 64 + 256), through the drop-in registry path, where no oracle runs: size-independent
@@ -834,7 +837,7 @@ def test_lego256_two_pass_vs_oracle(pkg, precision):
     mf, _ = build_mlp(pkg, LEGO_ARCH, 6, precision=precision)
     rm = EmissionAbsorptionRaymarcher(bg_color=(0.0, 0.0, 0.0), blend_output=False,
                                       background_density_bias=1e-6).to(DEV)
-    tol_rgb, tol_d = (1e-5, 1e-4) if precision != "bf16" else (3e-2, 0.25)
+    tol_rgb, tol_d = (1e-5, 1e-4) if not precision.startswith("bf16") else (3e-2, 0.25)
     with torch.no_grad():
         fc, dc, _, wc, _ = rm(**mc(t(o), t(d), t(z)), ray_lengths=t(z), ray_directions=t(d))
         close(n(fc), ref["coarse"][0], tol_rgb)
@@ -848,7 +851,7 @@ def test_lego256_two_pass_vs_oracle(pkg, precision):
     assert np.abs(ref["fine"][0]).max() > 1e-3, "degenerate case: the fine stage renders nothing"
 
 
-@pytest.mark.parametrize("precision", FP32_MODES + ["bf16"])
+@pytest.mark.parametrize("precision", FP32_MODES + ["bf16", "bf16s"])
 def test_lego256_mlp_gradients_vs_oracle(pkg, golden, precision):
     """NeRFMLP forward + backward at 320 points per ray (32 rays, 10,240 points) against the oracle's backward.
     At this many points a few pre-activations sit within round-off of zero and flip their ReLU mask between the GPU
@@ -873,7 +876,7 @@ def test_lego256_mlp_gradients_vs_oracle(pkg, golden, precision):
         v, r = n(p.grad).astype(np.float64), np.asarray(ref[name], np.float64).reshape(p.shape)
         rel = np.linalg.norm(v - r) / max(np.linalg.norm(r), 1e-12)
         print(f"{precision} grad {name}: rel L2 {rel:.2e}, max {np.abs(v - r).max() / np.abs(r).max():.2e} of max")
-        if precision == "bf16":
+        if precision.startswith("bf16"):
             assert rel <= bf16_grad_bound(golden), name  # the reference's own bf16 error x BF16_VS_AUTOCAST
         else:
             assert rel <= 5e-3, name
@@ -884,7 +887,7 @@ def test_lego256_mlp_gradients_vs_oracle(pkg, golden, precision):
                 assert rel <= 1e-4, (name, rel)
 
 
-@pytest.mark.parametrize("precision", FP32_MODES + ["bf16"])
+@pytest.mark.parametrize("precision", FP32_MODES + ["bf16", "bf16s"])
 @pytest.mark.parametrize("R,P", [(37, 100), (19, 64), (5, 200), (3, 50), (17, 65)])
 def test_colour_direction_gradient_ragged(pkg, golden, precision, R, P):
     """The colour layer's direction columns, which the fp32 backward sums by rays (dZc summed per ray, times the
@@ -912,7 +915,7 @@ def test_colour_direction_gradient_ragged(pkg, golden, precision, R, P):
     for key, cols in (("dir", slice(hid, None)), ("hid", slice(0, hid))):
         rel[key] = np.linalg.norm(w[:, cols] - r[:, cols]) / np.linalg.norm(r[:, cols])
         print(f"{precision} R={R} P={P} colour {key} columns: rel L2 {rel[key]:.2e}")
-    if precision == "bf16":
+    if precision.startswith("bf16"):
         assert rel["dir"] <= bf16_grad_bound(golden), rel
         return
     assert rel["dir"] <= 5e-3, rel

@@ -271,7 +271,8 @@ def test_trainer_trajectory_matches_reference(golden, precision):
 BF16_VS_AUTOCAST = 2.0  # as tests/test_gpu_parity.py: bf16 bounded by the reference's own bf16 error, x2
 
 
-def test_trainer_trajectory_bf16_within_the_references_own_bf16(golden):
+@pytest.mark.parametrize("precision", ["bf16", "bf16s"])
+def test_trainer_trajectory_bf16_within_the_references_own_bf16(golden, precision):
     """The bf16 throughput mode over the same 20-step trajectory (train_trajectory.npz's draws injected, its own
     refinement), against the reference's OWN bf16 trajectory (train_trajectory_bf16ref.npz: the reference's 20 steps on
     the same draws under torch.autocast("cpu", bfloat16)): every step's objective within BF16_VS_AUTOCAST x the
@@ -281,7 +282,7 @@ def test_trainer_trajectory_bf16_within_the_references_own_bf16(golden):
     from yanerf_amd import ops
     g, gb = golden("train_trajectory"), golden("train_trajectory_bf16ref")
     R, hw, K = int(g["n_rays"]), int(g["hw"]), int(g["steps"])
-    tr = make_trainer("bf16", g["seeds"], n_rays=R, hw=hw, runner_cfg=lego_cfg().runner)
+    tr = make_trainer(precision, g["seeds"], n_rays=R, hw=hw, runner_cfg=lego_cfg().runner)
     focal = t(g["focal"])
     losses = []
     for k in range(K):
@@ -308,12 +309,12 @@ def test_trainer_trajectory_bf16_within_the_references_own_bf16(golden):
         report.update({f"{key}_ours_vs_exact_l2": l2(ours), f"{key}_autocast_vs_exact_l2": l2(ac),
                        f"{key}_ours_vs_exact_max": mx(ours), f"{key}_autocast_vs_exact_max": mx(ac)})
         ok &= l2(ours) <= BF16_VS_AUTOCAST * l2(ac) and mx(ours) <= BF16_VS_AUTOCAST * mx(ac)
-    print(f"bf16 trajectory vs the reference's own bf16: {report}")
-    write_report("train_trajectory", "bf16 vs reference autocast", report)
+    print(f"{precision} trajectory vs the reference's own bf16: {report}")
+    write_report("train_trajectory", f"{precision} vs reference autocast", report)
     assert ok, report
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "bf16s"])
 def test_trainer_step_matches_registry_step(golden, precision):
     """The fused step and the drop-in registry path (NeRFPipeline + autograd) on the same injected draws: same kernels,
     so the gradients agree to float round-off (the registry path is the one test_gpu_parity pins to the reference)."""
@@ -452,7 +453,7 @@ def test_adam_matches_torch_adam(wd):
             assert torch.equal(a, b), (name, step, eq)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp32x3"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp32x3", "bf16s"])
 def test_pack_multi_equals_separate_packs(precision):
     """yanerf_mlp_pack_multi (both of the trainer's models in one launch) writes exactly the bytes of one
     yanerf_mlp_pack per model -- two Lego-size MLPs, a pair of different architectures (8 layers with a skip, and
@@ -671,7 +672,7 @@ def test_graph_replayed_steps_equal_eager_steps(precision):
     assert torch.equal(a["sq_fine"], b["sq_fine"]) and torch.equal(eager.flat.data, graph.flat.data)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "bf16s"])
 def test_backward_schedules_give_identical_steps(precision):
     """The trainer's backward schedules differ only in WHEN the coarse MLP backward runs: serial (after the fine one, on
     the compute stream), "early" (on the side stream right after the coarse composite, beside the refinement and the fine

@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 OUT="$GRAFT_REPO_ROOT/gpurun_out"
 [ -n "${SKIP_KT:-}" ] || timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_kt" -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras --psnr-steps 0 > "$OUT/${TAG}_kt.log" 2>&1 || exit $?
-for P in fp32 bf16 fp32x3; do
+for P in fp32 bf16 fp32x3 bf16s; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 600 rocprofv3 --pmc $C -d "$OUT/${TAG}_${P}_$C" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extras --psnr-steps 0 --secondary none --precision $P > "$OUT/${TAG}_${P}_$C.log" 2>&1 || exit $?
   done

@@ -90,4 +90,5 @@ def main(R=4096, P=192, reps=10):
 
 
 if __name__ == "__main__":
-    main()
+    import os
+    main(R=int(os.environ.get("YANERF_MB_R", 4096)), P=int(os.environ.get("YANERF_MB_P", 192)))

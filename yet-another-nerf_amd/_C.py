@@ -28,6 +28,7 @@ def source_id() -> str:
 PREC_F32 = 0
 PREC_BF16 = 1
 PREC_F32X3 = 2  # fp32 as three bf16 terms, six bf16 MFMAs per product (include/yanerf_hip.h)
+PREC_BF16S = 3  # bf16 with bf16 storage throughout (no fp8 sections; include/yanerf_hip.h)
 
 # every symbol include/yanerf_hip.h declares (checked by tests/test_capi.py)
 EXPORTS = (

@@ -96,6 +96,7 @@ struct MlpLayout {
   int64_t bint_off, bc_off, wd_off, bd_off, wo_off, bo_off;
   int64_t f_elems;
   int64_t bytes;
+  int s16;  // YANERF_PREC_BF16S: point-major sections and gradient rows in bf16 (no fp8)
 };
 
 // saved activation rows (each row_ld(Npad) elements of T)
@@ -146,10 +147,11 @@ template <typename T> __host__ __device__ constexpr int mask_w() {
 template <typename T> __host__ __device__ inline int64_t trunk_mask_words(int64_t Npad) {
   return Npad / Cfg<T>::M * Cfg<T>::WAVES * 64 * mask_w<T>();
 }
+static bool prec_bf16(int prec);
 static int64_t trunk_mask_words_prec(int prec, int64_t Npad) {
-  return prec == YANERF_PREC_F32    ? trunk_mask_words<float>(Npad)
-         : prec == YANERF_PREC_BF16 ? trunk_mask_words<bf16_t>(Npad)
-                                    : trunk_mask_words<x3_t>(Npad);
+  return prec == YANERF_PREC_F32 ? trunk_mask_words<float>(Npad)
+         : prec_bf16(prec)       ? trunk_mask_words<bf16_t>(Npad)
+                                 : trunk_mask_words<x3_t>(Npad);
 }
 __device__ __forceinline__ int64_t mask_index(int64_t Npad, int slot, int64_t pt16, int ft) {
   return (((int64_t)slot * (Npad / 16) + pt16) * 16 + ft) * 4;
@@ -174,68 +176,72 @@ constexpr int PM_HB = 1;  // bytes per saved H / C element
 // Y (intermediate_linear's output, signed, the X operand of color_layer.0's weight gradient only) as fp8 e4m3 with a
 // power-of-two scale per 128-point tile, like the backward's gradient rows
 constexpr int PM_YB = 1;
+// YANERF_PREC_BF16S (s16): the same point-major sections, all bf16 (H, Y, C, and the gradient rows: 2 bytes)
+__host__ __device__ constexpr int pm_hb(bool s16) { return s16 ? 2 : PM_HB; }
+__host__ __device__ constexpr int pm_yb(bool s16) { return s16 ? 2 : PM_YB; }
 struct PmSave {
   int64_t pe, h0, y, dpe, c, ysc, total;
 };
-__host__ __device__ inline PmSave pm_save(int L, int64_t Npad) {
+__host__ __device__ inline PmSave pm_save(int L, int64_t Npad, bool s16 = false) {
   PmSave s;
   int64_t o = 0;
   s.pe = o; o += 2LL * KPE * Npad;
-  s.h0 = o; o += (int64_t)PM_HB * 256 * L * Npad;
-  s.y = o; o += (int64_t)PM_YB * 256 * Npad;
+  s.h0 = o; o += (int64_t)pm_hb(s16) * 256 * L * Npad;
+  s.y = o; o += (int64_t)pm_yb(s16) * 256 * Npad;
   s.dpe = o; o += 2LL * KDIR * Npad;
-  s.c = o; o += (int64_t)PM_HB * HC * Npad;
+  s.c = o; o += (int64_t)pm_hb(s16) * HC * Npad;
   s.ysc = o; o += 4LL * (Npad / 128);
   s.total = (o + 255) / 256 * 256;
   return s;
 }
 // byte offset and element bytes of the saved section that starts at SavedRows row r0 (point-major bf16 layout)
-static int64_t pm_sec_bytes(int L, int64_t Npad, int64_t r0, int* es, int64_t* scale_off = nullptr) {
+static int64_t pm_sec_bytes(int L, int64_t Npad, int64_t r0, int* es, int64_t* scale_off = nullptr, bool s16 = false) {
   const SavedRows SR = saved_rows(L);
-  const PmSave PS = pm_save(L, Npad);
+  const PmSave PS = pm_save(L, Npad, s16);
   *es = 2;
   if (r0 == SR.pe) return PS.pe;
   if (r0 >= SR.h0 && r0 < SR.y) {
-    *es = PM_HB;
-    return PS.h0 + (r0 - SR.h0) / 256 * (int64_t)PM_HB * 256 * Npad;
+    *es = pm_hb(s16);
+    return PS.h0 + (r0 - SR.h0) / 256 * (int64_t)pm_hb(s16) * 256 * Npad;
   }
   if (r0 == SR.y) {
-    *es = PM_YB;
-    if (scale_off) *scale_off = PS.ysc;
+    *es = pm_yb(s16);
+    if (scale_off && !s16) *scale_off = PS.ysc;
     return PS.y;
   }
   if (r0 == SR.dpe) return PS.dpe;
-  *es = PM_HB;
+  *es = pm_hb(s16);
   return PS.c;  // r0 == SR.c
 }
 constexpr int PM_GB = 1;  // bytes per dZ / dY / dZc element in the bf16 backward workspace (fp8 e4m3, scaled)
+__host__ __device__ constexpr int pm_gb(bool s16) { return s16 ? 2 : PM_GB; }
 // bf16 backward workspace (point-major): byte offsets of the gradient sections, the dU section (bf16: du_j at column j,
 // dsigma at PM_DSIG) and the per-(section, 128-point tile) fp8 scales (float; sections dZ_0..dZ_{L-1}, dY, dZc)
 struct PmGrad {
   int64_t dz0, dy, dzc, du, scale, total;
 };
-__host__ __device__ inline PmGrad pm_grad(int L, int64_t Npad) {
+__host__ __device__ inline PmGrad pm_grad(int L, int64_t Npad, bool s16 = false) {
   PmGrad g;
   int64_t o = 0;
-  g.dz0 = o; o += (int64_t)PM_GB * 256 * L * Npad;
-  g.dy = o; o += (int64_t)PM_GB * 256 * Npad;
-  g.dzc = o; o += (int64_t)PM_GB * HC * Npad;
+  g.dz0 = o; o += (int64_t)pm_gb(s16) * 256 * L * Npad;
+  g.dy = o; o += (int64_t)pm_gb(s16) * 256 * Npad;
+  g.dzc = o; o += (int64_t)pm_gb(s16) * HC * Npad;
   g.du = o; o += 2LL * 16 * Npad;
   g.scale = o; o += 4LL * (L + 2) * (Npad / 128);
   g.total = (o + 255) / 256 * 256;
   return g;
 }
 // byte offset, element bytes and scale array (or null) of the gradient section starting at GradRows row r0
-static int64_t pm_grad_sec(int L, int64_t Npad, int64_t r0, int* es, int64_t* scale_off) {
+static int64_t pm_grad_sec(int L, int64_t Npad, int64_t r0, int* es, int64_t* scale_off, bool s16 = false) {
   const GradRows GR = grad_rows(L, true);
-  const PmGrad PG = pm_grad(L, Npad);
-  *es = PM_GB;
+  const PmGrad PG = pm_grad(L, Npad, s16);
+  *es = pm_gb(s16);
   *scale_off = -1;
   int sec;
   int64_t off;
   if (r0 >= GR.dz0 && r0 < GR.dyx) {
     sec = (int)((r0 - GR.dz0) / 256);
-    off = PG.dz0 + (int64_t)sec * PM_GB * 256 * Npad;
+    off = PG.dz0 + (int64_t)sec * pm_gb(s16) * 256 * Npad;
   } else if (r0 == GR.dyx) {
     sec = L;
     off = PG.dy;
@@ -246,21 +252,23 @@ static int64_t pm_grad_sec(int L, int64_t Npad, int64_t r0, int* es, int64_t* sc
     *es = 2;
     return PG.du;
   }
-  *scale_off = PG.scale + 4LL * sec * (Npad / 128);
+  if (!s16) *scale_off = PG.scale + 4LL * sec * (Npad / 128);
   return off;
 }
 // backward workspace bytes before the dW slabs
-static int64_t grad_t_bytes(int L, int64_t Npad, size_t es, bool pm) {
-  if (pm) return pm_grad(L, Npad).total;
+static int64_t grad_t_bytes(int L, int64_t Npad, size_t es, bool pm, bool s16 = false) {
+  if (pm) return pm_grad(L, Npad, s16).total;
   return grad_rows(L).rows * row_ld(Npad, es) * (int64_t)es;
 }
-static int64_t saved_t_bytes(int L, int64_t Npad, size_t es, bool pm) {
-  if (pm) return pm_save(L, Npad).total;
+static int64_t saved_t_bytes(int L, int64_t Npad, size_t es, bool pm, bool s16 = false) {
+  if (pm) return pm_save(L, Npad, s16).total;
   return saved_rows(L).rows * row_ld(Npad, es) * (int64_t)es;
 }
 
+// the bf16 kernels serve both bf16 precisions (YANERF_PREC_BF16S only changes the storage of the saved sections)
+static bool prec_bf16(int prec) { return prec == YANERF_PREC_BF16 || prec == YANERF_PREC_BF16S; }
 static int64_t tile_m(int prec) {
-  return prec == YANERF_PREC_F32 ? Cfg<float>::M : prec == YANERF_PREC_BF16 ? Cfg<bf16_t>::M : Cfg<x3_t>::M;
+  return prec == YANERF_PREC_F32 ? Cfg<float>::M : prec_bf16(prec) ? Cfg<bf16_t>::M : Cfg<x3_t>::M;
 }
 // Npad: a multiple of the point tile, so every workgroup holds a whole tile
 static int64_t npad_of(int prec, int64_t n) {
@@ -268,12 +276,12 @@ static int64_t npad_of(int prec, int64_t n) {
   return (n + M - 1) / M * M;
 }
 // element size of the saved activations / gradient rows (fp32 for both fp32 modes)
-static size_t elem_size(int prec) { return prec == YANERF_PREC_BF16 ? 2 : 4; }
+static size_t elem_size(int prec) { return prec_bf16(prec) ? 2 : 4; }
 // element size and plane count of the packed GEMM operands
 static size_t w_size(int prec) { return prec == YANERF_PREC_F32 ? 4 : 2; }
 static int w_planes(int prec) { return prec == YANERF_PREC_F32X3 ? 3 : 1; }
 static bool prec_pm(int prec) {
-  return prec == YANERF_PREC_F32 ? Cfg<float>::PM : prec == YANERF_PREC_BF16 ? Cfg<bf16_t>::PM : Cfg<x3_t>::PM;
+  return prec == YANERF_PREC_F32 ? Cfg<float>::PM : prec_bf16(prec) ? Cfg<bf16_t>::PM : Cfg<x3_t>::PM;
 }
 
 static int check_desc(const yanerf_mlp_desc* d) {
@@ -334,6 +342,7 @@ static MlpLayout make_layout(const yanerf_mlp_desc* d, int prec) {
   L.bo_off = f; f += CMAX;
   L.f_elems = f;
   L.bytes = L.f_base + f * 4;
+  L.s16 = prec == YANERF_PREC_BF16S;
   return L;
 }
 
@@ -1195,6 +1204,19 @@ __device__ __forceinline__ void save_grad_pm(const typename Cfg<T>::lds_t* act, 
   copy_tile_pm_fp8<T, NTHR, W, false, 2>(act, 0, (uint8_t*)dst, tid, sc);
 }
 
+// YANERF_PREC_BF16S: the same sections stay bf16 -- the LDS tile copied as it is (copy_tile_pm), no fp8 scales
+template <typename T, int NTHR, int W, bool S16>
+__device__ __forceinline__ void save_act_pm(const typename Cfg<T>::lds_t* act, char* dst, int tid) {
+  if constexpr (S16) copy_tile_pm<T, NTHR, W>(act, 0, (typename Cfg<T>::st_t*)dst, tid);
+  else save_relu_pm<T, NTHR, W>(act, 0, dst, tid);
+}
+template <typename T, int NTHR, int W, bool S16>
+__device__ __forceinline__ void save_grad_rows_pm(const typename Cfg<T>::lds_t* act, char* dst, float* scale_out,
+                                                  const float* red, int waves, int tid) {
+  if constexpr (S16) copy_tile_pm<T, NTHR, W>(act, 0, (typename Cfg<T>::st_t*)dst, tid);
+  else save_grad_pm<T, NTHR, W>(act, dst, scale_out, red, waves, tid);
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global stores (the
 // saved rows / gradients / masks written between barriers are read by later kernels only). __syncthreads() is a
 // workgroup fence as well and waits for every outstanding store (vmcnt(0)) at each of the ~24 barriers per tile.
@@ -1205,7 +1227,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // are separate instantiations, so the saves' presence is known at compile time: with a run-time saved-pointer test the
 // compiler waited vmcnt(0) at the next GEMM's first weight use, i.e. for the epilogue's stores too (x3 training forward
 // 4.97 -> 4.86 ms, fp32 7.57 -> 7.52 ms, bitwise equal).
-template <typename T, bool SAVE>
+template <typename T, bool SAVE, bool S16 = false>
 __global__ void __launch_bounds__(Cfg<T>::WAVES * 64)
     __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_fwd_kernel(
     MlpLayout lay, const typename Cfg<T>::w_t* __restrict__ Wt, const float* __restrict__ Wf,
@@ -1231,7 +1253,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64)
   constexpr bool sv = SAVE;
   const int64_t wpl = lay.t_plane;
   const SavedRows SR = saved_rows(lay.L);
-  const PmSave PS = pm_save(lay.L, Npad);  // byte offsets of the point-major sections (bf16)
+  const PmSave PS = pm_save(lay.L, Npad, S16);  // byte offsets of the point-major sections (bf16)
+  constexpr int HB = pm_hb(S16), YB = pm_yb(S16);
   const int mt_ = tid / TPP, q = tid % TPP;
   const int64_t p = p0 + mt_;
   const int64_t pc = p < N ? p : N - 1;
@@ -1281,7 +1304,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64)
       if (l == 0) {
         copy_tile_pm<T, NTHR, KPE>(act, PE_COL, (ST*)((char*)saved + PS.pe) + p0 * KPE, tid);
       } else {
-        save_relu_pm<T, NTHR, 256>(act, 0, (char*)saved + PS.h0 + ((l - 1) * Npad + p0) * 256LL * PM_HB, tid);
+        save_act_pm<T, NTHR, 256, S16>(act, (char*)saved + PS.h0 + ((l - 1) * Npad + p0) * 256LL * HB, tid);
 #pragma unroll
         for (int w = 0; w < MW; ++w)
           masks[((((int64_t)(l - 1) * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
@@ -1337,7 +1360,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64)
   ARing<T, NTC> ringc;
   ring_fill<T, NTC>(ringc, Wt + lay.wc_off, wpl, KC, crow0, KC / KB, lane);
   if constexpr (PM && sv) {
-    save_relu_pm<T, NTHR, 256>(act, 0, (char*)saved + PS.h0 + ((lay.L - 1) * Npad + p0) * 256LL * PM_HB, tid);
+    save_act_pm<T, NTHR, 256, S16>(act, (char*)saved + PS.h0 + ((lay.L - 1) * Npad + p0) * 256LL * HB, tid);
 #pragma unroll
     for (int w = 0; w < MW; ++w)
       masks[((((int64_t)(lay.L - 1) * ntiles + tile) * WAVES + wave) * MW + w) * 64 + lane] = pbits[w];
@@ -1357,12 +1380,12 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64)
         const int m = 16 * mt + li;
         const Pk<T> h = pk_make<T>(v);
         pk_lds<T>(act, m, n, h);
-        if constexpr (PM) gmax.add(h);
+        if constexpr (PM && !S16) gmax.add(h);
         if constexpr (sv && !PM)
           pk_store_rows_b<T>((saved + (SR.y + nrow0 + 16 * nt) * ld + p0), soff, (int)ldb, 16 * mt * (int)sizeof(ST), h);
       }
     }
-    if constexpr (PM) {
+    if constexpr (PM && !S16) {
       static_assert(PE_COL + 32 + 2 * WAVES <= ROW, "Y scale slots");
       const float am = wave_max(gmax.value());
       if (sv && lane == 0) yred[wave] = am;
@@ -1381,8 +1404,8 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64)
     f4 accc[NTC][MT];
     gemm_lds<T, NTC, MT>(Wt + lay.wc_off, wpl, KC, crow0, act, 0, KC / KB, accc, lane, Wf + lay.bc_off, &ringc);
     if constexpr (PM && sv) {
-      save_grad_pm<T, NTHR, 256>(act, (char*)saved + PS.y + p0 * 256 * PM_YB, (float*)((char*)saved + PS.ysc) + tile,
-                                 yred, WAVES, tid);
+      save_grad_rows_pm<T, NTHR, 256, S16>(act, (char*)saved + PS.y + p0 * 256 * YB,
+                                           (float*)((char*)saved + PS.ysc) + tile, yred, WAVES, tid);
       copy_tile_pm<T, NTHR, KDIR>(act, PE_COL, (ST*)((char*)saved + PS.dpe) + p0 * KDIR, tid);
     }
     lds_barrier();
@@ -1426,7 +1449,7 @@ __global__ void __launch_bounds__(Cfg<T>::WAVES * 64)
       }
     }
   }
-  if constexpr (PM && sv) save_relu_pm<T, NTHR, HC>(act, 0, (char*)saved + PS.c + p0 * (int64_t)HC * PM_HB, tid);
+  if constexpr (PM && sv) save_act_pm<T, NTHR, HC, S16>(act, (char*)saved + PS.c + p0 * (int64_t)HC * HB, tid);
 }
 
 // ---- the colour layer's direction columns by rays (fp32). LinearWithRepeat (nerf_mlp.py) feeds every
@@ -1453,7 +1476,7 @@ template <> __device__ __forceinline__ float lds_val<x3_t>(const bf16_t* act, in
 }
 
 // ============================================================================================ backward dX
-template <typename T>
+template <typename T, bool S16 = false>
 __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64)
     __attribute__((amdgpu_waves_per_eu(Cfg<T>::WPE))) mlp_bwd_dx_kernel(
     MlpLayout lay, const typename Cfg<T>::w_t* __restrict__ Wt, const float* __restrict__ Wf,
@@ -1488,12 +1511,13 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64)
   // the colour-output weights (PE columns of row 16), two sets used alternately: a set is rewritten only after the
   // barrier that follows the copy reading it
   [[maybe_unused]] char* const gb = (char*)grad;
-  [[maybe_unused]] const PmGrad PG = pm_grad(lay.L, Npad);
+  [[maybe_unused]] const PmGrad PG = pm_grad(lay.L, Npad, S16);
+  constexpr int GB = pm_gb(S16);
   [[maybe_unused]] float* const g8red = (float*)(act + 16 * ROW + PE_COL);
   [[maybe_unused]] float* const g8scl = (float*)(gb + PG.scale) + tile;
   [[maybe_unused]] const int64_t ntile = Npad / M;
   auto g8_note = [&](int set, float amax) {  // this wave's |max| of the section being formed
-    if constexpr (PM) {
+    if constexpr (PM && !S16) {
       amax = wave_max(amax);
       if (lane == 0) g8red[8 * set + wave] = amax;
     }
@@ -1604,7 +1628,8 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64)
   // point-major gradients leave the LDS tile after the GEMM that reads them (and its next-ring loads): see the
   // forward's trunk loop on the shared, in-order vmcnt
   if constexpr (PM)
-    save_grad_pm<T, NTHR, HC>(act, gb + PG.dzc + p0 * HC * PM_GB, g8scl + (lay.L + 1) * ntile, g8red, WAVES, tid);
+    save_grad_rows_pm<T, NTHR, HC, S16>(act, gb + PG.dzc + p0 * HC * GB, g8scl + (lay.L + 1) * ntile, g8red, WAVES,
+                                        tid);
   if (dzc_part) {
     // per-ray sums of dZc over this thread's chunk of the tile (column c), for the dirPE weight gradient by rays
     constexpr int CH = dzc_chunk<T>();
@@ -1636,7 +1661,7 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64)
       const int m = 16 * mt + li;
       f4 v = acc[nt][mt];
       const Pk<T> h = pk_make<T>(v);
-      if constexpr (PM) gmax.add(h);
+      if constexpr (PM && !S16) gmax.add(h);
       pk_lds<T>(act, m, n, h);
       if constexpr (!PM && !GSX)  // else stored by the first trunk step's GEMM
         pk_store_rows_b<T>((grad + (GR.dyx + nrow0 + 16 * nt) * ld + p0),
@@ -1664,10 +1689,11 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64)
     // fp8 scale sets: dZc 0, dY 1, then dZ_{L-1}, dZ_{L-2}, ... alternate from set 0
     if constexpr (PM) {  // the GEMM's input: dY (from the heads) or dZ_l
       if constexpr (HEAD)
-        save_grad_pm<T, NTHR, 256>(act, gb + PG.dy + p0 * 256 * PM_GB, g8scl + lay.L * ntile, g8red + 8, WAVES, tid);
+        save_grad_rows_pm<T, NTHR, 256, S16>(act, gb + PG.dy + p0 * 256 * GB, g8scl + lay.L * ntile, g8red + 8, WAVES,
+                                             tid);
       else
-        save_grad_pm<T, NTHR, 256>(act, gb + PG.dz0 + ((int64_t)l * Npad + p0) * 256 * PM_GB, g8scl + l * ntile,
-                                   g8red + 8 * ((lay.L + 1 - l) & 1), WAVES, tid);
+        save_grad_rows_pm<T, NTHR, 256, S16>(act, gb + PG.dz0 + ((int64_t)l * Npad + p0) * 256 * GB, g8scl + l * ntile,
+                                             g8red + 8 * ((lay.L + 1 - l) & 1), WAVES, tid);
     }
     lds_barrier();
     G8Max gmax;
@@ -1686,7 +1712,7 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64)
         }
         // ReLU mask of H_{hl}: this lane's own bits of this tile (packed by the forward)
         const Pk<T> h = pk_make<T>(apply_mask_tile<T, MW>(v, bits, nt * MT + mt));
-        if constexpr (PM) gmax.add(h);
+        if constexpr (PM && !S16) gmax.add(h);
         pk_lds<T>(act, m, n, h);
         if constexpr (!PM)
           if (!GSX || hl == 0)
@@ -1700,7 +1726,8 @@ __global__ void __launch_bounds__(Cfg<T>::DXWAVES * 64)
   trunk_step(std::integral_constant<bool, true>{}, lay.L);
   for (int l = lay.L - 1; l >= 1; --l) trunk_step(std::integral_constant<bool, false>{}, l);
   if constexpr (PM)
-    save_grad_pm<T, NTHR, 256>(act, gb + PG.dz0 + p0 * 256 * PM_GB, g8scl, g8red + 8 * ((lay.L + 1) & 1), WAVES, tid);
+    save_grad_rows_pm<T, NTHR, 256, S16>(act, gb + PG.dz0 + p0 * 256 * GB, g8scl, g8red + 8 * ((lay.L + 1) & 1), WAVES,
+                                         tid);
 }
 
 // ============================================================================================ backward dW
@@ -1761,7 +1788,9 @@ struct DwJobs {
 constexpr int DW_THREADS = 512;
 // widest dW column tile: bf16 is HBM/L2-bound (a 256-wide tile reads each dZ row once), fp32 is MFMA-bound and
 // runs faster with 128-wide tiles (measured: fp32 dW 8.3 ms vs 11.0 ms at 256; bf16 1.66 vs 2.0 ms at 128)
-__host__ __device__ constexpr int dw_bkmax(int prec) { return prec == YANERF_PREC_BF16 ? 256 : 128; }
+__host__ __device__ constexpr int dw_bkmax(int prec) {
+  return (prec == YANERF_PREC_BF16 || prec == YANERF_PREC_BF16S) ? 256 : 128;
+}
 template <typename T> constexpr int prec_of = YANERF_PREC_BF16;
 template <> constexpr int prec_of<float> = YANERF_PREC_F32;
 template <> constexpr int prec_of<x3_t> = YANERF_PREC_F32X3;
@@ -1793,6 +1822,7 @@ constexpr int PM_SPTS = 64;   // bf16: two stacked 32-point K-blocks per LDS-DMA
 static int64_t dw_stage_pts(int prec) {
   if (prec == YANERF_PREC_F32X3) return X3_SPTS;
   if (prec == YANERF_PREC_BF16) return PM_SPTS;
+  if (prec == YANERF_PREC_BF16S) return 32;  // bf16 images: a 256 x 256 tile's 32-point stage fills PM_STAGE_BYTES
   return Cfg<float>::KB * (DW_CPR / 4);
 }
 __device__ __forceinline__ int dw_swz4(int row, int c) { return c ^ (((row >> 3) & 1) << 1); }  // 64-byte rows (x3)
@@ -2045,7 +2075,7 @@ __device__ __forceinline__ int pm_swz(int r) {
   if constexpr (ROWB == 128) return 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
   else return 2 * ((r & 3) | (((r >> 3) & 1) << 2));
 }
-constexpr int PM_KBS = PM_SPTS / 32;  // 32-point K-blocks per stage (images stacked)
+
 // stage buffer: the widest image pair (A + X, 64 points) of any instantiation (256-row fp8 A + 256-column fp8 X)
 constexpr int PM_STAGE_BYTES = 32 * 1024;
 // LDS-DMA ring depth of the point-major (bf16) dW tile: as many stages as fit 128 KB (2 / 3 stages so that two
@@ -2146,22 +2176,24 @@ __device__ __forceinline__ i32x8 f8m_frag(const char* img, int f0, int lane) {
 }
 // e8m0 exponent of a power-of-two float scale
 __device__ __forceinline__ int e8m0_of(float s) { return (int)((__float_as_uint(s) >> 23) & 0xffu); }
-template <int BN, int BK, bool X8, bool A8>
+template <int BN, int BK, bool X8, bool A8, int SP = PM_SPTS>
 constexpr bool use_f8mma() {
-  return X8 && A8 && BK == 256 && (BN == 256 || BN == 128) && PM_SPTS == 64;
+  return X8 && A8 && BK == 256 && (BN == 256 || BN == 128) && SP == 64;
 }
 
-template <int BN, int BK, bool X8, bool A8>
+// SP: points per stage -- PM_SPTS (64) for the fp8 tiles, 32 for YANERF_PREC_BF16S, whose bf16 256 x 256 tile images
+// (16 KB + 16 KB per 32 points) would not fit a 32 KB stage at 64 points
+template <int BN, int BK, bool X8, bool A8, int SP = PM_SPTS>
 __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S, int64_t Npad, float* __restrict__ slab,
                                            int64_t slab_elems, char* smem) {
   constexpr int WN = BN / 64, WK0 = 8 / WN, WK = (BK / 16 < WK0) ? BK / 16 : WK0, KTW = BK / WK / 16;
   static_assert(KTW >= 1 && WN * WK <= 8, "dW wave tiling");
-  constexpr bool F8M = use_f8mma<BN, BK, X8, A8>();
+  constexpr bool F8M = use_f8mma<BN, BK, X8, A8, SP>();
   constexpr int XEB = X8 ? 1 : 2, RBX = BK * XEB;             // X element bytes, X image row bytes
   constexpr int AEB = A8 ? 1 : 2, RBA = BN * AEB;
-  constexpr int SPT = Cfg<bf16_t>::M / PM_SPTS;  // stages per fp8 scale tile
-  static_assert(SPT * PM_SPTS == Cfg<bf16_t>::M, "an fp8 scale covers whole dW stages");
-  constexpr int AB = PM_SPTS * RBA, XB = PM_SPTS * RBX;       // image bytes
+  constexpr int SPT = Cfg<bf16_t>::M / SP;  // stages per fp8 scale tile
+  static_assert(SPT * SP == Cfg<bf16_t>::M, "an fp8 scale covers whole dW stages");
+  constexpr int AB = SP * RBA, XB = SP * RBX;       // image bytes
   constexpr int NI = (AB + XB + 1023) / 1024, PW = (NI + 7) / 8;  // DMA wave-instructions per stage / per wave
   static_assert((AB + XB) % 1024 == 0, "pm dW images: whole DMA wave-instructions");
   static_assert(PW * 8 * 1024 <= PM_STAGE_BYTES, "pm dW stage");
@@ -2170,7 +2202,7 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
   const int g = lane >> 4, li = lane & 15;
   const int wn = wave / WK, wk = wave % WK;
   const bool mma_wave = wave < WN * WK;
-  const int64_t nst = Npad / PM_SPTS;
+  const int64_t nst = Npad / SP;
   const int64_t st_lo = nst * s / S, st_hi = nst * (s + 1) / S;
   // this lane's DMA source per wave-instruction and its per-stage advance (32 points of its section), in bytes
   const char* src[PW];
@@ -2187,7 +2219,7 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
       else if constexpr (A8) c = ((b % RBA) / 16) ^ pm_swz8<RBA>(r);
       else c = ((b % RBA) / 16) ^ pm_swz<RBA>(r);
       src[i] = (const char*)J.A + (int64_t)r * J.a_ld * AEB + 16 * (c < J.a_chunks ? c : 0);
-      adv[i] = (int64_t)PM_SPTS * J.a_ld * AEB;
+      adv[i] = (int64_t)SP * J.a_ld * AEB;
     } else if (b < AB + XB) {
       const int bx = b - AB, r = bx / RBX;
       int c;
@@ -2197,13 +2229,13 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
       const int j = k0 + (16 / XEB) * c;  // virtual column
       if (j < J.x0p) {
         src[i] = (const char*)J.X0 + ((int64_t)r * J.x0_ld + j) * x0b;
-        adv[i] = (int64_t)PM_SPTS * J.x0_ld * x0b;
+        adv[i] = (int64_t)SP * J.x0_ld * x0b;
       } else if (j - J.x0p < J.x1_ld && J.X1) {
         src[i] = (const char*)J.X1 + ((int64_t)r * J.x1_ld + (j - J.x0p)) * x1b;
-        adv[i] = (int64_t)PM_SPTS * J.x1_ld * x1b;
+        adv[i] = (int64_t)SP * J.x1_ld * x1b;
       } else {  // past the virtual width: any valid address (never stored)
         src[i] = (const char*)J.X0 + (int64_t)r * J.x0_ld * x0b;
-        adv[i] = (int64_t)PM_SPTS * J.x0_ld * x0b;
+        adv[i] = (int64_t)SP * J.x0_ld * x0b;
       }
     } else {  // padding of the last wave-instruction: a valid source into unused LDS
       src[i] = (const char*)J.A;
@@ -2326,7 +2358,7 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
     if (st + PM_STAGES - 1 < st_hi) issue(st + PM_STAGES - 1);
     const char* buf = smem + ((int)st % PM_STAGES) * PM_STAGE_BYTES;
 #pragma unroll
-    for (int kb = 0; kb < PM_KBS; ++kb)
+    for (int kb = 0; kb < SP / 32; ++kb)
     if (mma_wave) {
       // K-block kb of the stage: 32-point images at kb * 32 rows (the row swizzles repeat every 16 rows)
       const char* bufa = buf + kb * 32 * RBA;
@@ -2530,18 +2562,18 @@ __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S,
 
 // stage bytes of a point-major dW tile; the dispatch below only instantiates the tiles that fit PM_STAGE_BYTES (the
 // host checks every job's tiles against the same function before the launch)
-__host__ __device__ constexpr int pm_tile_bytes(int bn, int bk, bool x8, bool a8) {
-  return PM_SPTS * (bn * (a8 ? 1 : 2) + bk * (x8 ? 1 : 2));
+__host__ __device__ constexpr int pm_tile_bytes(int bn, int bk, bool x8, bool a8, int sp = PM_SPTS) {
+  return sp * (bn * (a8 ? 1 : 2) + bk * (x8 ? 1 : 2));
 }
-template <int BN, int BK, bool X8, bool A8>
+template <int BN, int BK, bool X8, bool A8, int SP = PM_SPTS>
 __device__ __forceinline__ void run_pm(const DwJob& J, int k0, int s, int S, int64_t Npad, float* __restrict__ slab,
                                        int64_t slab_elems, char* smem) {
-  if constexpr (pm_tile_bytes(BN, BK, X8, A8) <= PM_STAGE_BYTES)
-    dw_tile_pm<BN, BK, X8, A8>(J, k0, s, S, Npad, slab, slab_elems, smem);
+  if constexpr (pm_tile_bytes(BN, BK, X8, A8, SP) <= PM_STAGE_BYTES)
+    dw_tile_pm<BN, BK, X8, A8, SP>(J, k0, s, S, Npad, slab, slab_elems, smem);
   // else: not instantiated; launch_bwd refuses a job with such a tile before the launch
 }
 
-template <typename T>
+template <typename T, bool S16 = false>
 __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t Npad, float* __restrict__ slab) {
   // x3: two buffers of three 384-row bf16 planes (144 KB); otherwise the LDS-DMA ring
   __shared__ __attribute__((aligned(16))) char smem[is_x3<T>      ? 2 * 3 * 384 * 64
@@ -2572,7 +2604,22 @@ __global__ void __launch_bounds__(DW_THREADS) mlp_dw_kernel(DwJobs jobs, int64_t
   const int k0 = kt * BKMAX;
   const int bk = kt < J.k_full ? BKMAX : J.bk_tail;
   const int64_t se = jobs.slab_stride;
-  if constexpr (Cfg<T>::PM) {
+  if constexpr (Cfg<T>::PM && S16) {
+    // YANERF_PREC_BF16S: every operand bf16, 32-point stages, the bf16 MFMA (the dU rows' 64-row tiles as in the fp8 mode)
+    constexpr int SP = 32;
+    if (J.bn == 256) {
+      if (bk == 256) run_pm<256, 256, false, false, SP>(J, k0, s, S, Npad, slab, se, smem);
+      else if (bk == 128) run_pm<256, 128, false, false, SP>(J, k0, s, S, Npad, slab, se, smem);
+      else run_pm<256, 64, false, false, SP>(J, k0, s, S, Npad, slab, se, smem);
+    } else if (J.bn == 128) {
+      if (bk == 256) run_pm<128, 256, false, false, SP>(J, k0, s, S, Npad, slab, se, smem);
+      else if (bk == 128) run_pm<128, 128, false, false, SP>(J, k0, s, S, Npad, slab, se, smem);
+      else run_pm<128, 64, false, false, SP>(J, k0, s, S, Npad, slab, se, smem);
+    } else {
+      if (bk == 256) run_pm<64, 256, false, false, SP>(J, k0, s, S, Npad, slab, se, smem);
+      else run_pm<64, 128, false, false, SP>(J, k0, s, S, Npad, slab, se, smem);
+    }
+  } else if constexpr (Cfg<T>::PM) {
     // the tile's X format: fp8 if its columns come from an fp8 section (a k-tile never mixes formats: host check)
     const bool x8 = (k0 < J.x0p) ? J.x0_u8 : J.x1_u8;
     // and its A format: the 128 / 256-row tiles are fp8 gradient sections, a 64-row tile is a narrow fp8 gradient
@@ -2821,9 +2868,12 @@ static int build_pack_jobs(const yanerf_mlp_desc* d, const MlpLayout& L, int pre
 // rounds) 0.84-0.86, 16 0.82-0.83, 24 / 28 0.90-0.98 (profiles/r4_ab_bf16_dw_splits.jsonl)
 constexpr int DW_SMAX = 64;
 constexpr int DW_CUS = 256;  // MI355X compute units
-static int dw_splits(int total_tiles, int64_t n_stages, bool pm) {
+static int dw_splits(int total_tiles, int64_t n_stages, bool pm, bool s16 = false) {
   int64_t S;
-  if (pm) {
+  if (pm && s16) {  // no fp8 scales to fit: one round of one workgroup per CU
+    S = DW_CUS / total_tiles > 0 ? DW_CUS / total_tiles : 1;
+    if (S > n_stages) S = n_stages;
+  } else if (pm) {
     const int64_t cap = (int64_t)(Cfg<bf16_t>::M / PM_SPTS) * (PM_SCALES - 2);  // stages per split whose scales fit
     const int64_t need = (n_stages + cap - 1) / cap;
     const int64_t per_round = DW_CUS / total_tiles > 0 ? DW_CUS / total_tiles : 1;
@@ -2891,8 +2941,8 @@ static void for_each_dw_job(const MlpLayout& L, bool pm, F&& f, bool dir_by_ray 
 static int dw_x0p(const MlpLayout& L, bool pm, const DwSpec& sp) {
   if (!pm) return sp.x0_rows;
   int es = 2, es1 = 2;
-  pm_sec_bytes(L.L, 128, sp.x0, &es);
-  if (sp.x1 >= 0) pm_sec_bytes(L.L, 128, sp.x1, &es1);
+  pm_sec_bytes(L.L, 128, sp.x0, &es, nullptr, L.s16);
+  if (sp.x1 >= 0) pm_sec_bytes(L.L, 128, sp.x1, &es1, nullptr, L.s16);
   const int q = (sp.x1 >= 0 && es1 != es) ? dw_bkmax(YANERF_PREC_BF16) : (es == 1 ? 16 : 8);
   return (sp.x0_rows + q - 1) / q * q;
 }
@@ -2912,7 +2962,7 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
     if (r < 0) return nullptr;
     int b = 2;
     int64_t so = -1;
-    const int64_t off = pm_sec_bytes(L.L, Npad, r, &b, &so);
+    const int64_t off = pm_sec_bytes(L.L, Npad, r, &b, &so, L.s16);
     *u8 = b == 1;
     if (so >= 0) *scale = (const float*)((const char*)saved + so);
     return (const void*)((const char*)saved + off);
@@ -2921,7 +2971,7 @@ static void build_dw_jobs(const MlpLayout& L, int prec, const void* saved, void*
   int a_es = (int)es;  // point-major gradient section bytes per element (pm_grad)
   auto gsec = [&](int64_t r, const float** scale) -> const void* {
     int64_t so = -1;
-    const int64_t off = pm_grad_sec(L.L, Npad, r, &a_es, &so);
+    const int64_t off = pm_grad_sec(L.L, Npad, r, &a_es, &so, L.s16);
     *scale = so < 0 ? nullptr : (const float*)((const char*)gradbuf + so);
     return (const void*)((const char*)gradbuf + off);
   };
@@ -3056,7 +3106,15 @@ static int launch_fwd(const MlpLayout& L, int prec, const void* packed, const fl
   const float* Wf = (const float*)((const char*)packed + L.f_base);
   dim3 grid((unsigned)(Npad / Cfg<T>::M)), block(Cfg<T>::WAVES * 64);
   if (saved) {
-    uint64_t* masks = (uint64_t*)((char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM));
+    uint64_t* masks = (uint64_t*)((char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM, L.s16));
+    if constexpr (Cfg<T>::PM) {
+      if (L.s16) {
+        hipLaunchKernelGGL((mlp_fwd_kernel<T, true, true>), grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb,
+                           (ST*)saved, masks, Npad);
+        YN_LAUNCH_CHECK("mlp_forward");
+        return 0;
+      }
+    }
     hipLaunchKernelGGL((mlp_fwd_kernel<T, true>), grid, block, 0, st, L, Wt, Wf, o, d, t, R, P, sigma, rgb, (ST*)saved,
                        masks, Npad);
   } else
@@ -3076,12 +3134,12 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
   const typename Cfg<T>::w_t* Wt = (const typename Cfg<T>::w_t*)packed;
   const float* Wf = (const float*)((const char*)packed + L.f_base);
   ST* gradbuf = (ST*)ws;
-  const int64_t grad_bytes = grad_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM);
+  const int64_t grad_bytes = grad_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM, L.s16);
   float* slab = (float*)((char*)ws + grad_bytes);
   // the point splits and slab size are those of the full job set (yanerf_mlp_bwd_workspace_bytes)
   int tiles_all = 0;
   const int64_t slab_all = dw_slab_elems_for(L, prec, &tiles_all);
-  const int S = dw_splits(tiles_all, Npad / dw_stage_pts(prec), Cfg<T>::PM);
+  const int S = dw_splits(tiles_all, Npad / dw_stage_pts(prec), Cfg<T>::PM, L.s16);
   // the dirPE weight gradient by rays: per-ray dZc partials after the slabs, then the block partials
   constexpr int CH = dzc_chunk<T>();
   // (fp32 only, where it measured -0.21 ms of 15.2 ms per Lego fine backward; bf16 and fp32x3 gained less in dW than
@@ -3090,8 +3148,18 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
                           Npad < (1ll << 31);
   float* dzc_part = (float*)((char*)slab + (int64_t)S * slab_all * 4);
   float* blockp = dzc_part + 2 * (Npad / CH) * HC;
-  const uint64_t* masks = (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM));
+  const uint64_t* masks =
+      (const uint64_t*)((const char*)saved + saved_t_bytes(L.L, Npad, sizeof(ST), Cfg<T>::PM, L.s16));
   if (phase & 1) {
+    bool s16 = false;
+    if constexpr (Cfg<T>::PM) {
+      if (L.s16) {
+        hipLaunchKernelGGL((mlp_bwd_dx_kernel<T, true>), dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::DXWAVES * 64),
+                           0, st, L, Wt, Wf, masks, rgb, gs, gr, N, Npad, gradbuf, P, nullptr);
+        s16 = true;
+      }
+    }
+    if (!s16)
     hipLaunchKernelGGL(mlp_bwd_dx_kernel<T>, dim3((unsigned)(Npad / Cfg<T>::M)), dim3(Cfg<T>::DXWAVES * 64), 0, st, L,
                        Wt, Wf, masks, rgb, gs, gr, N, Npad, gradbuf, P, dir_by_ray ? dzc_part : nullptr);
     YN_LAUNCH_CHECK("mlp_backward_dx");
@@ -3111,16 +3179,23 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
         const DwJob& j = D.j[i];
         const int k0 = kt * dw_bkmax(prec), bk = kt < j.k_full ? dw_bkmax(prec) : j.bk_tail;
         const bool x8 = (k0 < j.x0p) ? j.x0_u8 : j.x1_u8;
-        YN_CHECK(pm_tile_bytes(j.bn, bk, x8, j.a_u8) <= PM_STAGE_BYTES,
+        YN_CHECK(pm_tile_bytes(j.bn, bk, x8, j.a_u8, L.s16 ? 32 : PM_SPTS) <= PM_STAGE_BYTES,
                  "mlp_backward: dW job %d k-tile %d needs %d B per stage (> %d)", i, kt,
-                 pm_tile_bytes(j.bn, bk, x8, j.a_u8), PM_STAGE_BYTES);
+                 pm_tile_bytes(j.bn, bk, x8, j.a_u8, L.s16 ? 32 : PM_SPTS), PM_STAGE_BYTES);
       }
   for (int i = 0; i < D.n; ++i)  // the dW tile's A format follows its row tile (dw_tile_pm's A8)
-    YN_CHECK(!Cfg<T>::PM || D.j[i].bn == 64 || D.j[i].a_u8,
+    YN_CHECK(!Cfg<T>::PM || D.j[i].bn == 64 || D.j[i].a_u8 != L.s16,
              "mlp_backward: dW job %d: gradient format %d does not match its %d-row tile", i, D.j[i].a_u8, D.j[i].bn);
   YN_CHECK(D.slab_stride <= dw_slab_pad(slab_all), "mlp_backward: dW slab larger than its workspace");
   if (dw) {
-    hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)D.total_wg), dim3(DW_THREADS), 0, st, D, Npad, slab);
+    bool s16 = false;
+    if constexpr (Cfg<T>::PM) {
+      if (L.s16) {
+        hipLaunchKernelGGL((mlp_dw_kernel<T, true>), dim3((unsigned)D.total_wg), dim3(DW_THREADS), 0, st, D, Npad, slab);
+        s16 = true;
+      }
+    }
+    if (!s16) hipLaunchKernelGGL(mlp_dw_kernel<T>, dim3((unsigned)D.total_wg), dim3(DW_THREADS), 0, st, D, Npad, slab);
     YN_LAUNCH_CHECK("mlp_backward_dw");
   }
   if (red) {
@@ -3129,7 +3204,7 @@ static int launch_bwd(const MlpLayout& L, int prec, const void* packed, const vo
     if (dir_by_ray) {
       const int gi = 2 * L.L + 4;  // color_layer.0 weight [hdir][hid + dir_dim]
       const SavedRows SR = saved_rows(L.L);
-      const PmSave PS = pm_save(L.L, Npad);
+      const PmSave PS = pm_save(L.L, Npad, L.s16);
       const bool pm = Cfg<T>::PM;
       const void* dpe = pm ? (const void*)((const char*)saved + PS.dpe)
                            : (const void*)((const char*)saved + SR.dpe * row_ld(Npad, sizeof(ST)) * sizeof(ST));
@@ -3166,7 +3241,7 @@ static int launch_pack(const PackJobs& J, int precision, void* stream) {
   dim3 grid((unsigned)((J.total / 4 + 255) / 256)), block(256);
   if (precision == YANERF_PREC_F32)
     hipLaunchKernelGGL(pack_kernel<float>, grid, block, 0, as_stream(stream), J);
-  else if (precision == YANERF_PREC_BF16)
+  else if (prec_bf16(precision))
     hipLaunchKernelGGL(pack_kernel<bf16_t>, grid, block, 0, as_stream(stream), J);
   else
     hipLaunchKernelGGL(pack_kernel<x3_t>, grid, block, 0, as_stream(stream), J);
@@ -3181,7 +3256,7 @@ int yanerf_mlp_pack(const yanerf_mlp_desc* d, int precision, const float* const*
 int yanerf_mlp_pack_multi(int n_models, const yanerf_mlp_desc* d, int precision, const float* const* const* params,
                           void* const* packed, void* stream) {
   YN_CHECK(n_models >= 1 && d && params && packed, "mlp_pack_multi: bad arguments");
-  YN_CHECK(precision == YANERF_PREC_F32 || precision == YANERF_PREC_BF16 || precision == YANERF_PREC_F32X3,
+  YN_CHECK(precision == YANERF_PREC_F32 || prec_bf16(precision) || precision == YANERF_PREC_F32X3,
            "mlp_pack: bad precision %d", precision);
   for (int m = 0; m < n_models; ++m) {
     if (check_desc(d + m)) return 1;
@@ -3209,7 +3284,7 @@ int yanerf_mlp_pack_multi(int n_models, const yanerf_mlp_desc* d, int precision,
 int64_t yanerf_mlp_saved_bytes(const yanerf_mlp_desc* d, int precision, int64_t n_points) {
   if (check_desc(d)) return -1;
   const int64_t Npad = npad_of(precision, n_points);
-  return saved_t_bytes(d->n_layers, Npad, elem_size(precision), prec_pm(precision)) +
+  return saved_t_bytes(d->n_layers, Npad, elem_size(precision), prec_pm(precision), precision == YANERF_PREC_BF16S) +
          (d->n_layers * trunk_mask_words_prec(precision, Npad) + mask_words_per_slot(Npad)) * 8;
 }
 
@@ -3217,13 +3292,14 @@ int64_t yanerf_mlp_bwd_workspace_bytes(const yanerf_mlp_desc* d, int precision, 
   if (check_desc(d)) return -1;
   MlpLayout L = make_layout(d, precision);
   const int64_t Npad = npad_of(precision, n_points);
-  const int64_t grad_bytes = grad_t_bytes(d->n_layers, Npad, elem_size(precision), prec_pm(precision));
+  const int64_t grad_bytes =
+      grad_t_bytes(d->n_layers, Npad, elem_size(precision), prec_pm(precision), precision == YANERF_PREC_BF16S);
   int tiles = 0;
   int64_t se = dw_slab_elems_for(L, precision, &tiles);
-  int S = dw_splits(tiles, Npad / dw_stage_pts(precision), prec_pm(precision));
+  int S = dw_splits(tiles, Npad / dw_stage_pts(precision), prec_pm(precision), precision == YANERF_PREC_BF16S);
   // + the per-ray dZc partials (two slots per dZc chunk) and the dirPE block partials (rays >= chunks when used)
   const int CH = precision == YANERF_PREC_F32 ? dzc_chunk<float>()
-                 : precision == YANERF_PREC_BF16 ? dzc_chunk<bf16_t>() : dzc_chunk<x3_t>();
+                 : prec_bf16(precision) ? dzc_chunk<bf16_t>() : dzc_chunk<x3_t>();
   const int64_t nblk = (Npad / CH + DIRB - 1) / DIRB + 1;
   return grad_bytes + (int64_t)S * se * 4 + (2 * (Npad / CH) * HC + nblk * HC * KDIR) * 4;
 }
@@ -3238,7 +3314,7 @@ int yanerf_mlp_dw_plan(const yanerf_mlp_desc* d, int precision, int64_t n_points
   int t = 0;
   dw_slab_elems_for(L, precision, &t);
   const int64_t nst = Npad / dw_stage_pts(precision);
-  const int S = dw_splits(t, nst, prec_pm(precision));
+  const int S = dw_splits(t, nst, prec_pm(precision), precision == YANERF_PREC_BF16S);
   *tiles = t;
   *splits = S;
   *stage_points = dw_stage_pts(precision);
@@ -3258,7 +3334,7 @@ int yanerf_mlp_forward(const yanerf_mlp_desc* d, int precision, const void* pack
   if (precision == YANERF_PREC_F32)
     return launch_fwd<float>(L, precision, packed, origins, directions, lengths, R, P, sigma_raw, rgb, saved,
                              as_stream(stream));
-  if (precision == YANERF_PREC_BF16)
+  if (prec_bf16(precision))
     return launch_fwd<bf16_t>(L, precision, packed, origins, directions, lengths, R, P, sigma_raw, rgb, saved,
                               as_stream(stream));
   if (precision == YANERF_PREC_F32X3)
@@ -3299,7 +3375,7 @@ int yanerf_mlp_backward_phase(const yanerf_mlp_desc* d, int precision, const voi
   if (precision == YANERF_PREC_F32)
     return launch_bwd<float>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R, P, grads, workspace,
                              as_stream(stream), phase);
-  if (precision == YANERF_PREC_BF16)
+  if (prec_bf16(precision))
     return launch_bwd<bf16_t>(L, precision, packed, saved, rgb, g_sigma, g_rgb, R, P, grads, workspace,
                               as_stream(stream), phase);
   if (precision == YANERF_PREC_F32X3)

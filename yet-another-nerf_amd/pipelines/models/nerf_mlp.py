@@ -16,7 +16,10 @@ from ... import _C, ops
 from .builder import MODELS
 from .utils import HarmonicEmbedding, LinearWithRepeat
 
-_PRECISIONS = {"fp32": _C.PREC_F32, "f32": _C.PREC_F32, "bf16": _C.PREC_BF16, "fp32x3": _C.PREC_F32X3}
+# bf16: bf16 MFMA with fp8 e4m3 storage of the saved activations / gradient rows (the throughput mode); bf16s: the same
+# bf16 MFMA kernels with every stored section bf16 (the precision of the reference under torch.autocast bf16)
+_PRECISIONS = {"fp32": _C.PREC_F32, "f32": _C.PREC_F32, "bf16": _C.PREC_BF16, "fp32x3": _C.PREC_F32X3,
+               "bf16s": _C.PREC_BF16S}
 
 
 def _xavier_init(linear) -> None:  # nerf_mlp.py:292-296

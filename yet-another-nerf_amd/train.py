@@ -152,7 +152,7 @@ class NeRFTrainer:
         # serial 3.590, both 3.648, split 3.613, early 3.548 -> bf16 defaults to "early" (the coarse backward beside
         # the refinement and the fine forward); fp32 serial 29.15 / early 29.15 / both 29.44 keeps serial.
         if overlap is None:
-            overlap = "early" if precision == "bf16" else False
+            overlap = "early" if precision in ("bf16", "bf16s") else False
         self.overlap = "both" if overlap is True else overlap
         self.side = torch.cuda.Stream(device=self.dev) if overlap else None
         # the gradient exchange runs whenever a process group is up (at world 1 too: bench.py's YANERF_PG_AT_WORLD1

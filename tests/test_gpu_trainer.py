@@ -829,3 +829,28 @@ def test_graph_render_advances_the_training_stream_like_render():
         graph.render_graph(pose, focal, 64, 64, chunk=1024)
     assert eager.rng.get_state() == graph.rng.get_state()
 
+
+
+def test_grad_exchange_auto_resolution():
+    """grad_exchange="auto" (the default): the two-bucket exchange for the Lego steps (4096 x 256 points), one
+    all-reduce below 2^19 points per step (the 1,024-ray Fern step; profiles/r6_exchange_world1.txt); explicit choices
+    and YANERF_GRAD_EXCHANGE are kept."""
+    import os
+
+    from yanerf_amd.train import NeRFTrainer
+    cfg = lego_cfg().pipeline
+    assert NeRFTrainer(cfg, precision="bf16", device=DEV).grad_exchange == "bucketed"
+    assert NeRFTrainer(cfg, precision="bf16", device=DEV, n_rays=1024).grad_exchange == "single"
+    assert NeRFTrainer(cfg, precision="bf16", device=DEV, n_rays=1024, grad_exchange="bucketed").grad_exchange == \
+        "bucketed"
+    old = os.environ.get("YANERF_GRAD_EXCHANGE")
+    os.environ["YANERF_GRAD_EXCHANGE"] = "bucketed"
+    try:
+        assert NeRFTrainer(cfg, precision="bf16", device=DEV, n_rays=1024).grad_exchange == "bucketed"
+    finally:
+        if old is None:
+            del os.environ["YANERF_GRAD_EXCHANGE"]
+        else:
+            os.environ["YANERF_GRAD_EXCHANGE"] = old
+    with pytest.raises(ValueError):
+        NeRFTrainer(cfg, precision="bf16", device=DEV, grad_exchange="ring")

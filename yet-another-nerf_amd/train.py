@@ -68,10 +68,13 @@ class NeRFTrainer:
         that many images at this world size and `batch_size`): num_iters and lr_decay_iters are rescaled, which at
         world > 1 changes the schedule. Without it the runner config is used as written (exact at world 1 when the
         train set divides num_iters).
-        grad_exchange (world > 1 only): "bucketed" (default) = one all-reduce per model, the coarse bucket started
-        right after the coarse MLP backward and overlapped with the fine one (this replaces the `overlap` schedule,
-        which only applies at world 1); "single" = one all-reduce of the whole flat gradient after both backwards
-        (the plain DDP-equivalent fallback). Env YANERF_GRAD_EXCHANGE sets the default. Both give the same sums.
+        grad_exchange (world > 1 only): "bucketed" = one all-reduce per model, the coarse bucket started right after the
+        coarse MLP backward and overlapped with the fine one; "single" = one all-reduce of the whole flat gradient
+        after both backwards (the plain DDP-equivalent); "auto" (default) = bucketed for steps of at least
+        BUCKETED_MIN_POINTS points (the Lego steps), single below (the 1,024-ray Fern step, where the second bucket's
+        launches and stream hand-offs cost more than its overlap saves: measured over RCCL at world size 1, Fern bf16
+        +6 % bucketed vs +2.5 % single against no process group, profiles/r6_exchange_world1.txt). Env
+        YANERF_GRAD_EXCHANGE sets the default. Every choice gives the same sums.
         seed: the weights are initialised from `seed` on every rank (then broadcast from rank 0, as DDP does); the
         trainer's own Philox stream (pixel sampling, jitter, density noise, refinement) is keyed by seed + rank,
         as scripts/run.py:70-71 seeds each rank. torch's global generator is left untouched."""
@@ -159,9 +162,11 @@ class NeRFTrainer:
         # rehearsal runs the N-rank schedule, collectives included, on one card)
         self.exchange = parallel.is_dist()
         self._h_early = None  # the coarse bucket's all-reduce, started on the side stream ("early")
-        self.grad_exchange = grad_exchange or os.environ.get("YANERF_GRAD_EXCHANGE", "bucketed")
+        self.grad_exchange = grad_exchange or os.environ.get("YANERF_GRAD_EXCHANGE", "auto")
+        if self.grad_exchange == "auto":
+            self.grad_exchange = "bucketed" if self.R * (self.Pc + self.Pf) >= self.BUCKETED_MIN_POINTS else "single"
         if self.grad_exchange not in ("bucketed", "single"):
-            raise ValueError(f"NeRFTrainer: grad_exchange {self.grad_exchange!r} (bucketed | single)")
+            raise ValueError(f"NeRFTrainer: grad_exchange {self.grad_exchange!r} (auto | bucketed | single)")
         self.grad_ptrs = [_C.ptr_array([p.grad.data_ptr() for p in ps]) for ps in self.params]
         self.param_ptrs = [_C.ptr_array([p.data_ptr() for p in ps]) for ps in self.params]
         # both models' packs in one launch (yanerf_mlp_pack_multi): the descriptors, the per-model parameter tables and
@@ -193,6 +198,7 @@ class NeRFTrainer:
         self._eval_ws: Dict[int, Dict[str, torch.Tensor]] = {}
 
     TAB_STEPS = 1024  # Adam schedule rows uploaded at a time
+    BUCKETED_MIN_POINTS = 1 << 19  # grad_exchange "auto": the two-bucket exchange from this many points per step
 
     def _pack(self, st):
         """Pack both models' current parameters into their kernel layouts: one launch when they share a precision."""

@@ -152,7 +152,9 @@ def _trainer_worker(rank, world, port, q):
     from yanerf_amd.utils.config import Config
     import yanerf_boot
     cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/lego.yml"))
-    tr = NeRFTrainer(cfg.pipeline, precision="fp32", device="cuda:0", n_rays=256, runner_cfg=cfg.runner, seed=42)
+    # the two-bucket exchange explicitly (at 256 rays grad_exchange="auto" would pick the single all-reduce)
+    tr = NeRFTrainer(cfg.pipeline, precision="fp32", device="cuda:0", n_rays=256, runner_cfg=cfg.runner, seed=42,
+                     grad_exchange="bucketed")
     local = []
     orig = parallel.allreduce_sum_async
 

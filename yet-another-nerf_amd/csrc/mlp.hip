@@ -2422,25 +2422,33 @@ __device__ __forceinline__ void dw_tile_pm(const DwJob& J, int k0, int s, int S,
 }
 
 // x3 dW: dZ and the layer inputs are fp32 rows in HBM (the x3 forward / dX save fp32). Each stage of 32 points is
-// loaded with 16-byte register loads (4 points of one row per thread-load, the next stage in flight while the
-// current one multiplies), split into three bf16 planes on the way into LDS (same 64-byte rows and swizzle as the
-// bf16 dW tile) and multiplied with the six plane products per 16x16x32 step. Two LDS buffers, one barrier per
-// stage. Bias gradients are fp32 row sums of the loaded dZ segments.
-// (A software-pipelined variant -- the next stage split while this one multiplies -- measured equal, round 3: the split
-// is not what the x3 dW waits on.)
+// loaded with 16-byte register loads (4 points of one row per thread-load), split into three bf16 planes on the way
+// into LDS (same 64-byte rows and swizzle as the bf16 dW tile) and multiplied with the six plane products per 16x16x32
+// step. Software pipelined over two LDS buffers with one barrier per stage: while a wave multiplies stage st from one
+// buffer it splits stage st + 1 (loaded during stage st - 1) into the other, one staged segment after each of the six
+// product terms, and reloads that segment's registers with stage st + 2 right away. The loop body is one basic block
+// (no per-segment branches: every staging slot is a real row, the last stage's split and reloads are harmless repeats),
+// so the split's VALU and LDS writes interleave with the MFMAs instead of running between two barriers with the
+// SIMD's matrix pipe idle (round 3's pipelined variant kept the per-segment branches and measured equal). Per
+// accumulator the stages and the six terms arrive in the same order: gradients bitwise equal to the unpipelined loop
+// (Lego fine dW 5.44-5.63 -> 4.95-5.15 ms; the alternatives measured in round 6 are in profiles/r6_x3_dw_ab.md).
+// Bias gradients are fp32 row sums of the loaded dZ segments.
 template <int BN, int BK>
 __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S, int64_t Npad,
                                            float* __restrict__ slab, int64_t slab_elems, char* smem) {
   constexpr int WN = BN / 64, WK0 = 8 / WN, WK = (BK / 16 < WK0) ? BK / 16 : WK0, KTW = BK / WK / 16;
-  static_assert(KTW >= 1 && WN * WK <= 8, "dW wave tiling");
-  constexpr int ROWS = BN + BK, LPT = (ROWS * 8 + DW_THREADS - 1) / DW_THREADS;  // 16-B loads per thread per stage
-  constexpr int PLB = 384 * 64, BUFB = 3 * PLB;                                  // plane / buffer bytes
+  static_assert(KTW >= 1 && KTW <= 4 && WN * WK == 8, "dW wave tiling: eight multiplying waves, one column group");
+  constexpr int ROWS = BN + BK;
+  static_assert(ROWS * 8 % DW_THREADS == 0, "x3 dW staging: whole 16-byte segments per thread");
+  constexpr int LPT = ROWS * 8 / DW_THREADS;  // 16-B loads per thread per stage; slot i holds row tid / 8 + 64 i
+  constexpr int LA = BN * 8 / DW_THREADS;     // slots 0 .. LA - 1 hold dZ rows (bias sums)
+  static_assert(LPT <= 6, "x3 dW pipeline: one staged segment per product term");
+  constexpr int PLB = 384 * 64, BUFB = 3 * PLB;  // plane / buffer bytes
   static_assert(ROWS <= 384, "x3 dW staging: at most 384 rows");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int wn = wave / WK, wk = wave % WK;
-  const bool mma_wave = wave < WN * WK;
   const int64_t nst = Npad / X3_SPTS, ld = row_ld(Npad, sizeof(float));
   const int64_t st_lo = nst * s / S, st_hi = nst * (s + 1) / S;
   const float* src[LPT];
@@ -2458,17 +2466,12 @@ __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S,
       else p = (const float*)J.X0;
     }
     src[i] = p + seg * 4;
-    dst[i] = row < ROWS ? row * 64 + (dw_swz4(row, seg >> 1) << 4) + (seg & 1) * 8 : -1;
+    dst[i] = row * 64 + (dw_swz4(row, seg >> 1) << 4) + (seg & 1) * 8;
   }
   f4 regs[LPT];
-  auto load = [&](int64_t st) {
+  float rsum[LA];
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) regs[i] = *(const f4*)(src[i] + st * X3_SPTS);
-  };
-  float rsum[LPT];
-#pragma unroll
-  for (int i = 0; i < LPT; ++i) rsum[i] = 0.f;
-  const bool do_bias = (k0 == 0);
+  for (int i = 0; i < LA; ++i) rsum[i] = 0.f;
   const f4 zero = f4{0.f, 0.f, 0.f, 0.f};
   f4 acc[4][KTW];
 #pragma unroll
@@ -2476,86 +2479,107 @@ __device__ __forceinline__ void dw_tile_x3(const DwJob& J, int k0, int s, int S,
 #pragma unroll
     for (int q = 0; q < KTW; ++q) acc[nt][q] = zero;
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  // split staged segment i (fp32) into the three bf16 planes of buffer `buf` (+ the bias row sums)
-  auto split_one = [&](int i, char* buf) {
-    if (dst[i] >= 0) {
-      const f4 v0 = regs[i];
-      if (do_bias && (tid + DW_THREADS * i) / 8 < BN) rsum[i] += (v0.x + v0.y) + (v0.z + v0.w);
-      const Pk<bf16_t> h0 = pk_make<bf16_t>(v0);
-      const f4 r1 = v0 - f4{__uint_as_float(h0.w0 << 16), __uint_as_float(h0.w0 & 0xffff0000u),
-                            __uint_as_float(h0.w1 << 16), __uint_as_float(h0.w1 & 0xffff0000u)};
-      const Pk<bf16_t> h1 = pk_make<bf16_t>(r1);
-      const f4 r2 = r1 - f4{__uint_as_float(h1.w0 << 16), __uint_as_float(h1.w0 & 0xffff0000u),
-                            __uint_as_float(h1.w1 << 16), __uint_as_float(h1.w1 & 0xffff0000u)};
-      const Pk<bf16_t> h2 = pk_make<bf16_t>(r2);
-      *(u32x2*)(buf + dst[i]) = u32x2{h0.w0, h0.w1};
-      *(u32x2*)(buf + PLB + dst[i]) = u32x2{h1.w0, h1.w1};
-      *(u32x2*)(buf + 2 * PLB + dst[i]) = u32x2{h2.w0, h2.w1};
+  // split staged segment i (fp32) into the three bf16 planes of buffer `buf` (+ the dZ row sums)
+  auto split_one = [&](int i, char* buf, bool sum) {
+    const f4 v0 = regs[i];
+    if (i < LA) {
+      const float r = rsum[i] + ((v0.x + v0.y) + (v0.z + v0.w));
+      rsum[i] = sum ? r : rsum[i];  // a select: the loop body stays one basic block
     }
+    const Pk<bf16_t> h0 = pk_make<bf16_t>(v0);
+    const f4 r1 = v0 - f4{__uint_as_float(h0.w0 << 16), __uint_as_float(h0.w0 & 0xffff0000u),
+                          __uint_as_float(h0.w1 << 16), __uint_as_float(h0.w1 & 0xffff0000u)};
+    const Pk<bf16_t> h1 = pk_make<bf16_t>(r1);
+    const f4 r2 = r1 - f4{__uint_as_float(h1.w0 << 16), __uint_as_float(h1.w0 & 0xffff0000u),
+                          __uint_as_float(h1.w1 << 16), __uint_as_float(h1.w1 & 0xffff0000u)};
+    const Pk<bf16_t> h2 = pk_make<bf16_t>(r2);
+    *(u32x2*)(buf + dst[i]) = u32x2{h0.w0, h0.w1};
+    *(u32x2*)(buf + PLB + dst[i]) = u32x2{h1.w0, h1.w1};
+    *(u32x2*)(buf + 2 * PLB + dst[i]) = u32x2{h2.w0, h2.w1};
   };
-  if (st_lo < st_hi) load(st_lo);
+  if (st_lo < st_hi) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) regs[i] = *(const f4*)(src[i] + st_lo * X3_SPTS);
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) split_one(i, smem + (int)(st_lo & 1) * BUFB, true);
+    const int64_t st1 = st_lo + 1 < st_hi ? st_lo + 1 : st_lo;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) regs[i] = *(const f4*)(src[i] + st1 * X3_SPTS);
+  }
+  lds_barrier();
+  // static priority for the second-dispatched half, the arbitration loser of each stage's start (5.12 -> 5.10 ms)
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  constexpr int TI[6] = {2, 1, 0, 1, 0, 0}, TJ[6] = {0, 1, 2, 0, 1, 0};
   for (int64_t st = st_lo; st < st_hi; ++st) {
-    char* buf = smem + (int)(st & 1) * BUFB;
-    // split the staged fp32 segments into the three planes of this stage's buffer
+    const char* buf = smem + (int)(st & 1) * BUFB;
+    char* nbuf = smem + (int)((st + 1) & 1) * BUFB;
+    const int64_t st2 = st + 2 < st_hi ? st + 2 : st_hi - 1;  // the last stages reload a valid stage (unused)
+    const bool nxt = st + 1 < st_hi;                           // the split of stage st + 1 is real
+    f4 a[3][4], b[3][KTW];
+    // the first term's operands (A plane 2, B plane 0) first
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) split_one(i, buf);
-    __syncthreads();
-    if (st + 1 < st_hi) load(st + 1);
-    if (mma_wave) {
-      f4 a[3][4];
+    for (int pl = 2; pl >= 0; --pl) {
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
+      for (int nt = 0; nt < 4; ++nt) {
+        const int row = wn * 64 + 16 * nt + li;
+        a[pl][nt] = *(const f4*)(buf + pl * PLB + row * 64 + (dw_swz4(row, g) << 4));
+      }
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const int row = wn * 64 + 16 * nt + li;
-          a[pl][nt] = *(const f4*)(buf + pl * PLB + row * 64 + (dw_swz4(row, g) << 4));
-        }
-      constexpr int QG = KTW < 4 ? KTW : 4;
-#pragma unroll
-      for (int q0 = 0; q0 < KTW; q0 += QG) {
-        f4 b[3][QG];
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-          for (int q = 0; q < QG; ++q) {
-            const int row = BN + (wk * KTW + q0 + q) * 16 + li;
-            b[pl][q] = *(const f4*)(buf + pl * PLB + row * 64 + (dw_swz4(row, g) << 4));
-          }
-        constexpr int TI[6] = {2, 1, 0, 1, 0, 0}, TJ[6] = {0, 1, 2, 0, 1, 0};
-#pragma unroll
-        for (int t = 0; t < 6; ++t)
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-            for (int q = 0; q < QG; ++q)
-              acc[nt][q0 + q] = mma_blk<bf16_t>(a[TI[t]][nt], b[TJ[t]][q], acc[nt][q0 + q]);
+      for (int q = 0; q < KTW; ++q) {
+        const int row = BN + (wk * KTW + q) * 16 + li;
+        b[2 - pl][q] = *(const f4*)(buf + (2 - pl) * PLB + row * 64 + (dw_swz4(row, g) << 4));
       }
     }
+    // one scheduling region per product term: its MFMAs, two VALU of the split after each, then the segment's three
+    // plane writes and its reload (the first region also carries the operand reads not needed by the first term)
+    constexpr int MT = 4 * KTW;  // MFMAs per term
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int q = 0; q < KTW; ++q) acc[nt][q] = mma_blk<bf16_t>(a[TI[t]][nt], b[TJ[t]][q], acc[nt][q]);
+      if (t < LPT) {
+        split_one(t, nbuf, nxt);
+        regs[t] = *(const f4*)(src[t] + st2 * X3_SPTS);
+      }
+      if (t == 0) __builtin_amdgcn_sched_group_barrier(0x100, 4 + KTW, 0);
+#pragma unroll
+      for (int j = 0; j < MT; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (t == 0 && j < 2 * (4 + KTW)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 32 / MT, 0);
+      }
+      if (t < LPT) {
+        __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    lds_barrier();
   }
   float* out = slab + (int64_t)s * slab_elems + J.slab_off;
   const int kv = J.ktot + 1;
-  if (mma_wave) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
+  for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-      for (int q = 0; q < KTW; ++q) {
-        const int k = k0 + (wk * KTW + q) * 16 + li;
+    for (int q = 0; q < KTW; ++q) {
+      const int k = k0 + (wk * KTW + q) * 16 + li;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int n = wn * 64 + 16 * nt + 4 * g + r;
-          if (n < J.a_rows && k < J.ktot) out[(int64_t)n * kv + k] = acc[nt][q][r];
-        }
+      for (int r = 0; r < 4; ++r) {
+        const int n = wn * 64 + 16 * nt + 4 * g + r;
+        if (n < J.a_rows && k < J.ktot) out[(int64_t)n * kv + k] = acc[nt][q][r];
       }
-  }
-  if (do_bias) {
+    }
+  if (k0 == 0) {
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
+    for (int i = 0; i < LA; ++i) {
       const int flat = tid + DW_THREADS * i, row = flat >> 3;
       float v = rsum[i];
       v += __shfl_xor(v, 1, 64);
       v += __shfl_xor(v, 2, 64);
       v += __shfl_xor(v, 4, 64);
-      if ((flat & 7) == 0 && row < BN && row < J.a_rows) out[(int64_t)row * kv + J.ktot] = v;
+      if ((flat & 7) == 0 && row < J.a_rows) out[(int64_t)row * kv + J.ktot] = v;
     }
   }
 }

@@ -1227,15 +1227,38 @@ def gen_train_step_lego256_4096(out):
     out["train_step_lego256_4096"] = _full_step(256, (91, 92), (-40.0, -25.0), 28, 29, relu_oracle=False)
 
 
-def _full_step(n_fine, seeds, view, img_seed, torch_seed, relu_oracle):
+FERN_FULL_RAYS = 1024  # fern.yml's n_rays_per_image_sampled_from_mask (BASELINE configs[3])
+
+
+def gen_train_step_fern_1024(out):
+    """BASELINE configs[3]'s training step (Fern 504 x 378, 64 + 128 samples, per-image (1, 1) depth bounds, no density
+    noise) at its full 1024 rays through the reference, as gen_train_step_lego256_4096: the draws (pixel ids, jitter,
+    refinement uniforms), depths, per-ray outputs, objective and gradients, and the float64 and bf16-autocast re-runs on
+    the same draws and depths."""
+    out["train_step_fern_1024"] = _full_step(128, (53, 54), (0.05,), 37, 38, relu_oracle=False, scene="fern")
+
+
+def _full_step(n_fine, seeds, view, img_seed, torch_seed, relu_oracle, scene="lego"):
     sys.path.insert(0, str(HERE.parents[1]))
     from oracle import nerf_oracle as O
-    R = FULL_RAYS
-    pcfg = lego_pipeline_cfg(n_fine=n_fine)
+    if scene == "lego":
+        R, H, W = FULL_RAYS, 800, 800
+        pcfg = lego_pipeline_cfg(n_fine=n_fine)
+        pose = torch.from_numpy(synthetic_pose(view[0], view[1], 4.0))[None]
+        focal = torch.tensor([1111.1111])
+        bounds = {}
+        draw_kinds = ["multinomial", "rand_like", "randn_like", "rand", "randn_like"]
+    else:
+        from scene import forward_pose
+        R, H, W = FERN_FULL_RAYS, 378, 504
+        pcfg = fern_pipeline_cfg(n_fine, R)
+        pose = torch.from_numpy(forward_pose(view[0]))[None]
+        focal = torch.tensor([FERN_FOCAL])
+        bounds = dict(min_depth=torch.tensor([[FERN_NEAR]]), max_depth=torch.tensor([[FERN_FAR]]))
+        draw_kinds = ["multinomial", "rand_like", "rand"]  # fern.yml: no density noise
+    tag = f"train_step_{scene}_{R}"
     assert int(pcfg.ray_sampler.n_rays_per_image_sampled_from_mask) == R
-    pose = torch.from_numpy(synthetic_pose(view[0], view[1], 4.0))[None]
-    focal = torch.tensor([1111.1111])
-    img = torch.rand(1, 800, 800, 3, generator=torch.Generator().manual_seed(img_seed))
+    img = torch.rand(1, H, W, 3, generator=torch.Generator().manual_seed(img_seed))
     Pc, Pf = 64, 64 + n_fine
 
     def build(dtype=torch.float32):
@@ -1276,21 +1299,25 @@ def _full_step(n_fine, seeds, view, img_seed, torch_seed, relu_oracle):
     torch.manual_seed(torch_seed)
     try:
         with rec.capture():
-            preds = pipe(poses=pose, focal_lengths=focal, image_rgb=img, evaluation_mode=EvaluationMode.TRAINING)
+            preds = pipe(poses=pose, focal_lengths=focal, image_rgb=img, evaluation_mode=EvaluationMode.TRAINING,
+                         **bounds)
     finally:
         RayPointRefiner.forward = orig_ref
         for h in hooks:
             h.remove()
     preds["objective"].mean().backward()
     kinds = [n for n, _ in rec.log]
-    assert kinds == ["multinomial", "rand_like", "randn_like", "rand", "randn_like"], kinds
+    assert kinds == draw_kinds, kinds
     ids = rec.log[0][1].numpy().astype(np.int64)
     z_fine = np32(refined[0][1]).reshape(R, Pf)
     fine_o, coarse_o = stage_out[-1], stage_out[-1].prev_stage
-    d = dict(pose=np32(pose), focal=np32(focal), seeds=np.array(seeds), n_rays=np.int64(R), H=np.int64(800),
-             W=np.int64(800), pixel_ids=ids, gt_rgb=np32(img.reshape(1, -1, 3)[0, ids[0]]),
-             jitter_u=np32(rec.log[1][1]), noise_coarse=np32(rec.log[2][1]), pdf_u=np32(rec.log[3][1]),
-             noise_fine=np32(rec.log[4][1]), coarse_weights=np32(refined[0][0]).reshape(R, Pc), z_fine=z_fine,
+    drawn = dict(jitter_u=np32(rec.log[1][1]), pdf_u=np32(rec.log[kinds.index("rand")][1]))
+    if "randn_like" in kinds:
+        drawn.update(noise_coarse=np32(rec.log[2][1]), noise_fine=np32(rec.log[4][1]))
+    d = dict(pose=np32(pose), focal=np32(focal), seeds=np.array(seeds), n_rays=np.int64(R), H=np.int64(H),
+             W=np.int64(W), pixel_ids=ids, gt_rgb=np32(img.reshape(1, -1, 3)[0, ids[0]]),
+             **{k: np32(v) for k, v in bounds.items()}, **drawn,
+             coarse_weights=np32(refined[0][0]).reshape(R, Pc), z_fine=z_fine,
              coarse_features=np32(coarse_o.features).reshape(R, 3), coarse_depths=np32(coarse_o.depths).reshape(R),
              fine_features=np32(fine_o.features).reshape(R, 3), fine_depths=np32(fine_o.depths).reshape(R),
              **({"tie_rel": np.float32(FULL_TIE_REL)} if relu_oracle else {}))
@@ -1319,7 +1346,7 @@ def _full_step(n_fine, seeds, view, img_seed, torch_seed, relu_oracle):
     put_grads("grad", pipe.implicit_functions)  # grad / gradidx / gradval / gradsum: the golden_grad_items layout
     log = list(rec.log)
     del pipe, preds, stage_out, fine_o, coarse_o
-    print("train_step_lego_4096: fp32 step recorded", flush=True)
+    print(f"{tag}: fp32 step recorded", flush=True)
 
     def rerun(dtype, autocast=False):
         """The same step on the recorded draws, the refined depths replaced by the fp32 reference's."""
@@ -1334,14 +1361,15 @@ def _full_step(n_fine, seeds, view, img_seed, torch_seed, relu_oracle):
 
             RayPointRefiner.forward = fixed
             try:
+                bd = {k: v.to(dtype) for k, v in bounds.items()}
                 with replay_draws(log):
                     if autocast:
                         with torch.autocast("cpu", dtype=torch.bfloat16):
                             pr = p2(poses=pose.to(dtype), focal_lengths=focal.to(dtype), image_rgb=img.to(dtype),
-                                    evaluation_mode=EvaluationMode.TRAINING)
+                                    evaluation_mode=EvaluationMode.TRAINING, **bd)
                     else:
                         pr = p2(poses=pose.to(dtype), focal_lengths=focal.to(dtype), image_rgb=img.to(dtype),
-                                evaluation_mode=EvaluationMode.TRAINING)
+                                evaluation_mode=EvaluationMode.TRAINING, **bd)
             finally:
                 RayPointRefiner.forward = orig_ref
             pr["objective"].mean().backward()
@@ -1353,12 +1381,12 @@ def _full_step(n_fine, seeds, view, img_seed, torch_seed, relu_oracle):
     put_grads("grad64_", p64.implicit_functions)
     d["objective_f64"] = np.float64(obj64)
     del p64
-    print("train_step_lego_4096: float64 re-run", flush=True)
+    print(f"{tag}: float64 re-run", flush=True)
     pbf, objbf = rerun(torch.float32, autocast=True)
     put_grads("grad_bf16ac", pbf.implicit_functions)
     d["objective_bf16ac"] = np.float64(objbf)
     del pbf
-    print("train_step_lego_4096: bf16 autocast re-run", flush=True)
+    print(f"{tag}: bf16 autocast re-run", flush=True)
 
     if not relu_oracle:
         return d
@@ -1409,7 +1437,7 @@ GENERATORS = (gen_harmonic, gen_raysampler, gen_mlp, gen_raymarcher, gen_sample_
               gen_train_step, gen_zero_outputer, gen_init_checksums, gen_pipeline_state, gen_lr_schedule,
               gen_raysampler_masked, gen_iter_runner, gen_render_fern, gen_train_step_fern, gen_sensitivity,
               gen_render_trained, gen_train_step_trained, gen_train_trajectory, gen_train_step_lego_4096,
-              gen_mlp_bf16ref, gen_train_trajectory_bf16ref, gen_train_step_lego256_4096)
+              gen_mlp_bf16ref, gen_train_trajectory_bf16ref, gen_train_step_lego256_4096, gen_train_step_fern_1024)
 
 
 def main():

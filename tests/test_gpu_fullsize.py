@@ -74,36 +74,60 @@ def state_of(g):
             for k, v in p.items()}
 
 
+def is_fern(g):
+    return "min_depth" in g  # configs[3]'s golden: per-image (1, 1) depth bounds
+
+
+def rays_of(g):
+    return int(g["n_rays"])
+
+
 def draws_of(g, depths=True):
-    d = dict(pixel_ids=t(g["pixel_ids"], torch.int64), jitter_u=t(g["jitter_u"]),
-             noise=[t(g["noise_coarse"]), t(g["noise_fine"])], pdf_u=t(g["pdf_u"]))
+    d = dict(pixel_ids=t(g["pixel_ids"], torch.int64), jitter_u=t(g["jitter_u"]), pdf_u=t(g["pdf_u"]))
+    if "noise_coarse" in g:  # fern.yml has no density noise
+        d["noise"] = [t(g["noise_coarse"]), t(g["noise_fine"])]
     if depths:
         d["z_fine"] = t(g["z_fine"])
     return d
 
 
 def target_image(g):
-    img = torch.zeros(1, HW, HW, 3, device=DEV)
+    img = torch.zeros(1, int(g["H"]), int(g["W"]), 3, device=DEV)
     img.view(1, -1, 3)[0, torch.as_tensor(g["pixel_ids"][0], device=DEV)] = t(g["gt_rgb"])
     return img
+
+
+def fern_cfg(n_fine):
+    import yanerf_boot
+    from yanerf_amd.utils.config import Config
+    cfg = Config.fromfile(str(yanerf_boot.PKG_DIR / "configs/nerf/fern.yml"))
+    cfg.pipeline.renderer.n_pts_per_ray_fine_training = cfg.pipeline.renderer.n_pts_per_ray_fine_evaluation = n_fine
+    return cfg
 
 
 def run_trainer(g, precision):
     from yanerf_amd import ops
     from yanerf_amd.train import NeRFTrainer
-    tr = NeRFTrainer(lego_cfg(n_fine_of(g)).pipeline, precision=precision, device=DEV)
-    assert tr.R == R and tr.Pc == PC and tr.Pf == PC + n_fine_of(g)  # lego.yml (configs[1]; configs[4]: 64 + 256)
+    cfg = fern_cfg(n_fine_of(g)) if is_fern(g) else lego_cfg(n_fine_of(g))
+    tr = NeRFTrainer(cfg.pipeline, precision=precision, device=DEV)
+    # lego.yml (configs[1]; configs[4]: 64 + 256) / fern.yml (configs[3]: 1024 rays, 64 + 128)
+    assert tr.R == rays_of(g) and tr.Pc == PC and tr.Pf == PC + n_fine_of(g)
     tr.load_pipeline_state_dict(state_of(g))
+    bounds = dict(near=t(g["min_depth"]), far=t(g["max_depth"])) if is_fern(g) else {}
     with ops.injected_randomness(**draws_of(g)):
-        out = tr.step(t(g["pose"]), t(g["focal"]), target_image(g))
+        out = tr.step(t(g["pose"]), t(g["focal"]), target_image(g), **bounds)
     torch.cuda.synchronize()
     return tr, out
 
 
-def dw_plans(spec, pf=PF):
+def step_objective(g, out):
+    return float((out["sq_fine"].sum() + out["sq_coarse"].sum()) / (rays_of(g) * 3))
+
+
+def dw_plans(spec, pf=PF, rays=R):
     from yanerf_amd import _C
-    return {"coarse": _C.dw_plan(spec.desc(), spec.precision, R * PC), "fine": _C.dw_plan(spec.desc(), spec.precision,
-                                                                                         R * pf)}
+    return {"coarse": _C.dw_plan(spec.desc(), spec.precision, rays * PC),
+            "fine": _C.dw_plan(spec.desc(), spec.precision, rays * pf)}
 
 
 # ------------------------------------------------------------------------------------------- ReLU decisions
@@ -234,7 +258,7 @@ def test_full_size_trainer_step_matches_reference(g4096, precision):
     weights, per-ray outputs, the float64 yardstick and the strict tie-budget gate on every golden gradient entry."""
     g = g4096
     tr, out = run_trainer(g, precision)
-    obj = float((out["sq_fine"].sum() + out["sq_coarse"].sum()) / (R * 3))
+    obj = step_objective(g, out)
     rep = dict(precision=precision, rays=R, points=R * (PC + PF), dw_plan=dw_plans(tr.specs[1]),
                objective_err=abs(obj - float(g["objective"][0])), reference_objective_err_vs_f64=abs(
                    float(g["objective"][0]) - float(g["objective_f64"])))
@@ -315,9 +339,9 @@ def bf16_vs_autocast(g, tag, precision="bf16"):
     """Our bf16 step (bf16 + fp8 storage, or bf16s: bf16 storage throughout) on the golden's draws and depths against
     the reference's fp32 and bf16-autocast gradients."""
     tr, out = run_trainer(g, precision)
-    obj = float((out["sq_fine"].sum() + out["sq_coarse"].sum()) / (R * 3))
+    obj = step_objective(g, out)
     ref_obj, ac_obj = float(g["objective"][0]), float(g["objective_bf16ac"])
-    rep = dict(dw_plan=dw_plans(tr.specs[1], tr.Pf), objective_err=abs(obj - ref_obj),
+    rep = dict(dw_plan=dw_plans(tr.specs[1], tr.Pf, rays_of(g)), objective_err=abs(obj - ref_obj),
                autocast_objective_err=abs(ac_obj - ref_obj))
     ratios, per = {}, {}
     for i, name, v, ref, idx in golden_grad_items(g, tr.models):
@@ -356,18 +380,38 @@ def test_configs4_full_size_step_matches_reference(g4096_256, precision):
     against the reference's own step (train_step_lego256_4096.npz): the fp32 modes by the objective (1e-6), the per-ray
     outputs and the float64 yardstick; bf16 (the mode configs[4] names, here bf16 + fp8 storage; its weight gradients in
     two rounds of 18 splits) within BF16_VS_AUTOCAST x the reference's own bf16-autocast error per gradient tensor."""
-    g = g4096_256
+    full_size_step_vs_reference(g4096_256, "configs[4]", precision)
+
+
+def full_size_step_vs_reference(g, tag, precision):
+    """The fp32 modes: objective (1e-6), coarse weights, per-ray fine outputs, the float64 yardstick; bf16 modes:
+    bf16_vs_autocast."""
     if precision.startswith("bf16"):
-        bf16_vs_autocast(g, "configs[4]", precision)
+        bf16_vs_autocast(g, tag, precision)
         return
     tr, out = run_trainer(g, precision)
-    obj = float((out["sq_fine"].sum() + out["sq_coarse"].sum()) / (R * 3))
-    rep = dict(precision=precision, dw_plan=dw_plans(tr.specs[1], tr.Pf),
+    obj = step_objective(g, out)
+    rep = dict(precision=precision, rays=rays_of(g), dw_plan=dw_plans(tr.specs[1], tr.Pf, rays_of(g)),
                objective_err=abs(obj - float(g["objective"][0])))
     assert rep["objective_err"] <= 1e-6, rep
     assert np.abs(n(tr.passes[0].w) - g["coarse_weights"]).max() <= 1e-5
+    np.testing.assert_allclose(n(tr.passes[0].feats), g["coarse_features"], atol=1e-5, rtol=0)
     np.testing.assert_allclose(n(tr.passes[1].feats), g["fine_features"], atol=1e-5, rtol=0)
     np.testing.assert_allclose(n(tr.passes[1].depth), g["fine_depths"], atol=1e-4, rtol=0)
-    rep.update(exact_report(g, tr.models, f"configs[4] {precision}"))
-    print(f"configs[4] full-size step {precision}: {rep}")
-    write_report("train_step_4096", f"configs[4] trainer {precision} depths=reference", rep)
+    rep.update(exact_report(g, tr.models, f"{tag} {precision}"))
+    print(f"{tag} full-size step {precision}: {rep}")
+    write_report("train_step_4096", f"{tag} trainer {precision} depths=reference", rep)
+
+
+@pytest.fixture(scope="module")
+def g1024_fern(golden):
+    return golden("train_step_fern_1024")
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3", "bf16", "bf16s"])
+def test_configs3_full_size_step_matches_reference(g1024_fern, precision):
+    """BASELINE configs[3]'s step (Fern 504 x 378, 64 + 128 samples, per-image (1, 1) depth bounds, 1024 rays: the
+    bench's extras.fern_64_128_train workload) at full size against the reference's own step
+    (train_step_fern_1024.npz), gated as configs[4]'s: the fp32 modes by the objective, the per-ray outputs and the
+    float64 yardstick; the bf16 modes within BF16_VS_AUTOCAST x the reference's own bf16-autocast error per tensor."""
+    full_size_step_vs_reference(g1024_fern, "configs[3]", precision)

@@ -397,3 +397,28 @@ def test_reference_and_oracle_fp32_gradients_vs_exact_algorithm(golden, case):
             worst_o32 = max(worst_o32, float(np.abs(o32 - e).max() / M))
         assert 1e-6 < worst_ref <= 5e-4, (i, worst_ref)
         assert 1e-6 < worst_o32 <= 5e-4, (i, worst_o32)
+
+
+def test_train_step_fern_1024_stagewise(golden):
+    """The oracle against BASELINE configs[3]'s full-size reference step (train_step_fern_1024.npz: fern.yml at 1024
+    rays, 64 + 128, (1, 1) depth bounds, no density noise): the training rays from the recorded pixel ids and jitter, the
+    coarse weights and both stages' features at the reference's refined depths, and the objective (the two stages'
+    mean squared errors) -- the golden's forward half pinned to the oracle, as train_step_fern_* is at 64 rays; and the
+    reference's fp32 objective against its own float64 re-run of the same draws."""
+    g = golden("train_step_fern_1024")
+    arch = O.MLPArch.from_dict(LEGO_ARCH)
+    pc, pf = (make_nerf_mlp_params(LEGO_ARCH, int(s)) for s in g["seeds"])
+    near, far = float(g["min_depth"].mean()), float(g["max_depth"].mean())
+    R, H, W = int(g["n_rays"]), int(g["H"]), int(g["W"])
+    o, d, t, _ = O.sample_rays_train(g["pose"], g["focal"], W, H, near, far, 64, g["pixel_ids"], g["jitter_u"])
+    cfg = O.RenderCfg(n_pts_fine=int(g["z_fine"].shape[-1]) - 64, near=near, far=far,
+                      raymarch=O.RaymarchOpts(background_density_bias=1e-6))
+    r = O.render_two_pass(pc, pf, arch, cfg, o.reshape(R, 3), d.reshape(R, 3), t.reshape(R, 64), z_fine=g["z_fine"])
+    np.testing.assert_allclose(r["coarse"][3], g["coarse_weights"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(r["coarse"][0], g["coarse_features"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(r["fine"][0], g["fine_features"], atol=1e-5, rtol=0)
+    gt = g["gt_rgb"].astype(np.float64)
+    obj = np.mean((np.asarray(r["fine"][0], np.float64) - gt) ** 2) + np.mean((np.asarray(r["coarse"][0], np.float64)
+                                                                               - gt) ** 2)
+    close(obj, g["objective"][0], 1e-6)
+    close(float(g["objective"][0]), float(g["objective_f64"]), 1e-6)

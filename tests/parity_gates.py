@@ -34,6 +34,19 @@ STRICT_GRAD = 1e-4  # north_star's fp32 bound, as max |ours - reference| / max |
 REPORTS = Path(os.environ.get("YANERF_PARITY_REPORTS", ROOT / "gpurun_out" / "parity_reports.jsonl"))
 
 
+
+# The bf16 mode stores the weight gradients' X operands H_0..H_7, Y and C as fp8 e4m3 (3 mantissa bits; the reference's
+# bf16 autocast keeps them bf16): a weight gradient formed from an fp8 X carries up to e4m3's unit roundoff 2^-4 of
+# relative error per term. With few effective points that shows: on mlp_lego's 256 points with random upstream
+# gradients the colour-output weights (0.035 vs the autocast's 0.0071), on configs[3]'s full-size step (1024 rays x 64
+# coarse points) the coarse layer-5 weights (0.0545 vs 0.0222); at configs[1]'s 786k fine points 0.0018 / 0.0043 vs
+# 0.0027 / 0.0043. So in the bf16 (fp8-storage) mode these tensors' bound is at least FP8_UNIT; the all-bf16 mode
+# (bf16s) keeps the autocast-derived bound alone.
+FP8_UNIT = 2.0 ** -4
+FP8_X_WEIGHTS = tuple(f"xyz_encoder.mlp.{i}.0.weight" for i in range(1, 8)) + (
+    "intermediate_linear.weight", "color_layer.0.weight", "color_layer.2.weight")
+
+
 def write_report(kind: str, tag: str, report: dict) -> None:
     """Append one JSON line {kind, tag, time, **report} to the parity report file."""
     try:

@@ -13,7 +13,7 @@ import pytest
 import torch
 
 from oracle import nerf_oracle as O
-from parity_gates import (TIE_REL, golden_grad_items, golden_relu_masks, hip_relu_masks, loose_grad_gate,
+from parity_gates import (FP8_UNIT, FP8_X_WEIGHTS, TIE_REL, golden_grad_items, golden_relu_masks, hip_relu_masks, loose_grad_gate,
                           oracle_fine_at, relu_ties, split_gate, summarize_tie_budget, tie_budget_gate, write_report)
 from weights import LEGO_ARCH, SMALL_ARCH, make_nerf_mlp_params
 
@@ -129,15 +129,7 @@ def test_mlp_fwd_bwd_fp32(pkg, golden, tag, precision):
 # autocast is, per output and per gradient tensor (or within BF16_FLOOR relative L2 where autocast is nearly exact)
 BF16_VS_AUTOCAST = 2.0
 BF16_FLOOR = 2e-2
-# ... and the bf16 mode stores the weight gradients' X operands H_0..H_7, Y and C as fp8 e4m3 (3 mantissa bits; the
-# autocast reference keeps them bf16): a weight gradient formed from an fp8 X carries up to e4m3's unit roundoff 2^-4
-# of relative error per term. On mlp_lego's 256 points with random upstream gradients that shows on the colour-output
-# weights (measured 0.035 vs the autocast's 0.0071; on the full-size training step, where the sums run over 786k points
-# of a real loss, 0.0018 / 0.0043 vs 0.0027 / 0.0043: tests/test_gpu_fullsize.py), so these tensors' bound is at least
-# FP8_UNIT.
-FP8_UNIT = 2.0 ** -4
-FP8_X_WEIGHTS = tuple(f"xyz_encoder.mlp.{i}.0.weight" for i in range(1, 8)) + (
-    "intermediate_linear.weight", "color_layer.0.weight", "color_layer.2.weight")
+# ... and the bf16 mode's fp8 e4m3 X operands: parity_gates.FP8_UNIT / FP8_X_WEIGHTS (shared with the full-size tests)
 
 
 def _rel_l2(v, ref):
